@@ -1,0 +1,498 @@
+// smfv_host.cpp -- host-side inputs: Matrix Market reader, glibc-rand fat
+// vector, synthetic CSR generators, SMFV binary containers (smfv_host.h).
+//
+// Reader semantics follow SC/utils.cpp:70-185; the fat vector follows
+// SC/utils.cpp:193-209.  Generators are counter-hash based so that any row
+// block (one GPU's shard) can be produced independently and in parallel.
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "smfv.h"
+#include "smfv_host.h"
+#include "smfv_internal.h"
+
+using smfv::set_error;
+
+namespace {
+
+inline uint64_t splitmix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+inline uint64_t hash3(uint64_t seed, uint64_t a, uint64_t b)
+{
+    return splitmix64(splitmix64(seed ^ splitmix64(a)) ^ b);
+}
+inline double u01(uint64_t h) { return (double)(h >> 11) * (1.0 / 9007199254740992.0); }
+
+int nthreads_for(int64_t work)
+{
+    unsigned hc = std::thread::hardware_concurrency();
+    int t = (int)std::min<unsigned>(hc ? hc : 1, 16u);
+    if (work < (1 << 16)) t = 1;
+    return std::max(1, t);
+}
+
+template <class F> void parallel_rows(int64_t begin, int64_t end, F f)
+{
+    const int nt = nthreads_for(end - begin);
+    if (nt == 1) {
+        f(begin, end);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int64_t chunk = (end - begin + nt - 1) / nt;
+    for (int t = 0; t < nt; ++t) {
+        const int64_t a = begin + t * chunk, b = std::min(end, a + chunk);
+        if (a >= b) break;
+        th.emplace_back(f, a, b);
+    }
+    for (auto &x : th) x.join();
+}
+
+template <class T> T *xmalloc(size_t count)
+{
+    return static_cast<T *>(std::malloc(sizeof(T) * (count ? count : 1)));
+}
+
+}  // namespace
+
+extern "C" {
+
+SMFV_API void smfv_free(void *p) { std::free(p); }
+
+// ---------------------------------------------------------------------------
+// glibc rand() stream, default seed 1 (TYPE_3: r[i] = r[i-3] + r[i-31])
+// ---------------------------------------------------------------------------
+SMFV_API void smfv_fatvector_rand(int64_t n, int K, double *X)
+{
+    int32_t r[34];
+    r[0] = 1;
+    for (int i = 1; i < 31; ++i) {
+        // 16807 * r[i-1] % (2^31 - 1) via Schrage, as glibc's srandom_r
+        const int32_t hi = r[i - 1] / 127773, lo = r[i - 1] % 127773;
+        int32_t w = 16807 * lo - 2836 * hi;
+        if (w < 0) w += 2147483647;
+        r[i] = w;
+    }
+    uint32_t ring[34];
+    for (int i = 0; i < 31; ++i) ring[i] = (uint32_t)r[i];
+    for (int i = 31; i < 34; ++i) ring[i] = ring[i - 31];
+    // r[i] for i >= 34 = r[i-31] + r[i-3]; outputs start at i = 344
+    int64_t idx = 34;
+    auto next = [&]() {
+        const uint32_t v = ring[(idx - 31) % 34] + ring[(idx - 3) % 34];
+        ring[idx % 34] = v;
+        ++idx;
+        return v;
+    };
+    while (idx < 344) next();
+    const int64_t total = n * (int64_t)K;
+    for (int64_t i = 0; i < total; ++i) X[i] = (double)((int32_t)(next() >> 1) % 100 + 1);
+}
+
+// ---------------------------------------------------------------------------
+// Matrix Market (SC/utils.cpp:70-185)
+// ---------------------------------------------------------------------------
+SMFV_API int smfv_mtx_read(const char *path, int *out_m, int *out_n, int64_t *out_nnz,
+                           int **out_rp, int **out_ci, double **out_va)
+{
+    SMFV_REQUIRE(path && out_m && out_n && out_nnz && out_rp && out_ci && out_va, "null argument");
+    FILE *f = std::fopen(path, "rb");
+    if (!f) {
+        set_error("Unable to open file: %s", path);
+        return SMFV_ERR_HOST;
+    }
+    std::string buf;
+    {
+        std::fseek(f, 0, SEEK_END);
+        long sz = std::ftell(f);
+        std::fseek(f, 0, SEEK_SET);
+        buf.resize(sz > 0 ? (size_t)sz : 0);
+        if (sz > 0 && std::fread(&buf[0], 1, (size_t)sz, f) != (size_t)sz) {
+            std::fclose(f);
+            set_error("read error: %s", path);
+            return SMFV_ERR_HOST;
+        }
+        std::fclose(f);
+    }
+    // comment / header lines: first char '%' (utils.cpp:84-105)
+    size_t pos = 0;
+    bool sym = false, pat = false;
+    std::string line;
+    bool have = false;
+    while (pos <= buf.size()) {
+        size_t nl = buf.find('\n', pos);
+        if (nl == std::string::npos) nl = buf.size();
+        line.assign(buf, pos, nl - pos);
+        pos = nl + 1;
+        if (!line.empty() && line[0] == '%') {
+            if (line.find("symmetric") != std::string::npos) sym = true;
+            if (line.find("pattern") != std::string::npos) pat = true;
+            continue;
+        }
+        have = true;
+        break;
+    }
+    long long m = -1, n = -1, nz = -1;
+    if (!have || std::sscanf(line.c_str(), "%lld %lld %lld", &m, &n, &nz) != 3 || m < 0 || n < 0 ||
+        nz < 0 || m > 0x7fffffff || n > 0x7fffffff) {
+        set_error("Failed to read matrix dimensions from file: %s", path);
+        return SMFV_ERR_HOST;
+    }
+    const int64_t cap = sym ? 2 * nz : nz;
+    std::vector<int> rows((size_t)cap);
+    std::vector<std::pair<int, double>> ent((size_t)cap);
+    const char *p = buf.c_str() + std::min(pos, buf.size());
+    int64_t t = 0;
+    for (long long i = 0; i < nz; ++i) {
+        char *endp;
+        errno = 0;
+        long r = std::strtol(p, &endp, 10);
+        if (endp == p) goto bad;
+        p = endp;
+        {
+            long c = std::strtol(p, &endp, 10);
+            if (endp == p) goto bad;
+            p = endp;
+            double v = 1.0;  // pattern (utils.cpp:130)
+            if (!pat) {
+                v = std::strtod(p, &endp);
+                if (endp == p) goto bad;
+                p = endp;
+            }
+            r -= 1;
+            c -= 1;  // 1-based -> 0-based (utils.cpp:143-144)
+            if (r < 0 || r >= m || c < 0 || c >= n) goto bad;
+            rows[t] = (int)r;
+            ent[t] = {(int)c, v};
+            ++t;
+            if (sym && r != c) {  // mirror (utils.cpp:149-152)
+                if (c >= m) goto bad;
+                rows[t] = (int)c;
+                ent[t] = {(int)r, v};
+                ++t;
+            }
+        }
+    }
+    {
+        int *rp = xmalloc<int>((size_t)m + 1);
+        int *ci = xmalloc<int>((size_t)t);
+        double *va = xmalloc<double>((size_t)t);
+        if (!rp || !ci || !va) {
+            std::free(rp);
+            std::free(ci);
+            std::free(va);
+            set_error("out of memory");
+            return SMFV_ERR_HOST;
+        }
+        std::vector<int64_t> cnt((size_t)m + 1, 0);
+        for (int64_t i = 0; i < t; ++i) cnt[(size_t)rows[i] + 1]++;
+        for (long long i = 0; i < m; ++i) cnt[i + 1] += cnt[i];
+        if (cnt[m] > 0x7fffffff) {
+            std::free(rp);
+            std::free(ci);
+            std::free(va);
+            set_error("nnz exceeds int32 row_ptr");
+            return SMFV_ERR_HOST;
+        }
+        std::vector<int64_t> fill(cnt.begin(), cnt.end() - 1);
+        std::vector<std::pair<int, double>> sorted((size_t)t);
+        for (int64_t i = 0; i < t; ++i) sorted[fill[rows[i]]++] = ent[i];
+        for (long long i = 0; i < m; ++i)  // per-row sort by (col, value) (utils.cpp:156-159)
+            std::sort(sorted.begin() + cnt[i], sorted.begin() + cnt[i + 1]);
+        for (long long i = 0; i <= m; ++i) rp[i] = (int)cnt[i];
+        for (int64_t i = 0; i < t; ++i) {
+            ci[i] = sorted[i].first;
+            va[i] = sorted[i].second;
+        }
+        *out_m = (int)m;
+        *out_n = (int)n;
+        *out_nnz = t;
+        *out_rp = rp;
+        *out_ci = ci;
+        *out_va = va;
+        return SMFV_OK;
+    }
+bad:
+    set_error("Failed to read data from file: %s", path);
+    return SMFV_ERR_HOST;
+}
+
+SMFV_API int smfv_mtx_write(const char *path, int m, int n, const int *rp, const int *ci,
+                            const double *va, int symmetric)
+{
+    SMFV_REQUIRE(path && rp && m >= 0 && n >= 0, "bad argument");
+    FILE *f = std::fopen(path, "w");
+    if (!f) {
+        set_error("cannot write %s", path);
+        return SMFV_ERR_HOST;
+    }
+    int64_t cnt = 0;
+    for (int i = 0; i < m; ++i)
+        for (int j = rp[i]; j < rp[i + 1]; ++j)
+            if (!symmetric || ci[j] <= i) ++cnt;
+    std::fprintf(f, "%%%%MatrixMarket matrix coordinate real %s\n", symmetric ? "symmetric" : "general");
+    std::fprintf(f, "%d %d %lld\n", m, n, (long long)cnt);
+    for (int i = 0; i < m; ++i)
+        for (int j = rp[i]; j < rp[i + 1]; ++j)
+            if (!symmetric || ci[j] <= i) std::fprintf(f, "%d %d %.17g\n", i + 1, ci[j] + 1, va[j]);
+    const bool ok = std::fclose(f) == 0;
+    if (!ok) {
+        set_error("write error on %s", path);
+        return SMFV_ERR_HOST;
+    }
+    return SMFV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// SMFV binary containers
+// ---------------------------------------------------------------------------
+SMFV_API int smfv_csr_write_bin(const char *path, int m, int n, const int *rp, const int *ci,
+                                const double *va)
+{
+    SMFV_REQUIRE(path && rp && m >= 0 && n >= 0, "bad argument");
+    FILE *f = std::fopen(path, "wb");
+    if (!f) {
+        set_error("cannot write %s", path);
+        return SMFV_ERR_HOST;
+    }
+    const int64_t nnz = rp[m];
+    bool ok = std::fwrite("SMFVCSR1", 1, 8, f) == 8 && std::fwrite(&m, 4, 1, f) == 1 &&
+              std::fwrite(&n, 4, 1, f) == 1 && std::fwrite(&nnz, 8, 1, f) == 1 &&
+              std::fwrite(rp, 4, (size_t)m + 1, f) == (size_t)m + 1 &&
+              (nnz == 0 || (std::fwrite(ci, 4, (size_t)nnz, f) == (size_t)nnz &&
+                            std::fwrite(va, 8, (size_t)nnz, f) == (size_t)nnz));
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok) {
+        set_error("write error on %s", path);
+        return SMFV_ERR_HOST;
+    }
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_csr_read_bin(const char *path, int *out_m, int *out_n, int64_t *out_nnz,
+                               int **out_rp, int **out_ci, double **out_va)
+{
+    SMFV_REQUIRE(path && out_m && out_n && out_nnz && out_rp && out_ci && out_va, "null argument");
+    FILE *f = std::fopen(path, "rb");
+    if (!f) {
+        set_error("Unable to open file: %s", path);
+        return SMFV_ERR_HOST;
+    }
+    char magic[8];
+    int32_t m = 0, n = 0;
+    int64_t nnz = 0;
+    bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, "SMFVCSR1", 8) == 0 &&
+              std::fread(&m, 4, 1, f) == 1 && std::fread(&n, 4, 1, f) == 1 &&
+              std::fread(&nnz, 8, 1, f) == 1 && m >= 0 && n >= 0 && nnz >= 0;
+    int *rp = nullptr, *ci = nullptr;
+    double *va = nullptr;
+    if (ok) {
+        rp = xmalloc<int>((size_t)m + 1);
+        ci = xmalloc<int>((size_t)nnz);
+        va = xmalloc<double>((size_t)nnz);
+        ok = rp && ci && va && std::fread(rp, 4, (size_t)m + 1, f) == (size_t)m + 1 &&
+             (nnz == 0 || (std::fread(ci, 4, (size_t)nnz, f) == (size_t)nnz &&
+                           std::fread(va, 8, (size_t)nnz, f) == (size_t)nnz));
+    }
+    std::fclose(f);
+    if (!ok) {
+        std::free(rp);
+        std::free(ci);
+        std::free(va);
+        set_error("bad SMFV CSR file %s", path);
+        return SMFV_ERR_HOST;
+    }
+    *out_m = m;
+    *out_n = n;
+    *out_nnz = nnz;
+    *out_rp = rp;
+    *out_ci = ci;
+    *out_va = va;
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_dense_write_bin(const char *path, int64_t rows, int64_t cols, const double *data)
+{
+    SMFV_REQUIRE(path && rows >= 0 && cols >= 0 && (rows * cols == 0 || data), "bad argument");
+    FILE *f = std::fopen(path, "wb");
+    if (!f) {
+        set_error("cannot write %s", path);
+        return SMFV_ERR_HOST;
+    }
+    bool ok = std::fwrite("SMFVDNS1", 1, 8, f) == 8 && std::fwrite(&rows, 8, 1, f) == 1 &&
+              std::fwrite(&cols, 8, 1, f) == 1 &&
+              (rows * cols == 0 || std::fwrite(data, 8, (size_t)(rows * cols), f) == (size_t)(rows * cols));
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok) {
+        set_error("write error on %s", path);
+        return SMFV_ERR_HOST;
+    }
+    return SMFV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// fem27: symmetric 27-point-stencil surrogate
+// ---------------------------------------------------------------------------
+SMFV_API int smfv_gen_fem27(int m, int nx, int ny, double keep, uint64_t seed, int64_t *out_nnz,
+                            int **out_rp, int **out_ci, double **out_va)
+{
+    SMFV_REQUIRE(m >= 0 && nx >= 3 && ny >= 3 && keep >= 0 && keep <= 1, "bad fem27 parameters");
+    SMFV_REQUIRE(out_nnz && out_rp && out_ci && out_va, "null argument");
+    const int64_t plane = (int64_t)nx * ny;
+    auto visit = [&](int64_t i, auto &&emit) {
+        const int64_t x = i % nx, y = (i / nx) % ny, z = i / plane;
+        for (int dz = -1; dz <= 1; ++dz)
+            for (int dy = -1; dy <= 1; ++dy)
+                for (int dx = -1; dx <= 1; ++dx) {
+                    if (x + dx < 0 || x + dx >= nx || y + dy < 0 || y + dy >= ny || z + dz < 0) continue;
+                    const int64_t j = i + dx + (int64_t)nx * dy + plane * dz;
+                    if (j < 0 || j >= m) continue;
+                    if (j == i) {
+                        emit(j, 1.0 + u01(hash3(seed, (uint64_t)i, (uint64_t)i)));
+                        continue;
+                    }
+                    const uint64_t a = (uint64_t)std::min(i, j), b = (uint64_t)std::max(i, j);
+                    const uint64_t h = hash3(seed, a, b);
+                    if (u01(h) < keep) emit(j, 2.0 * u01(splitmix64(h ^ 0xA5A5A5A5ull)) - 1.0);
+                }
+    };
+    std::vector<int64_t> cnt((size_t)m + 1, 0);
+    parallel_rows(0, m, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            int64_t c = 0;
+            visit(i, [&](int64_t, double) { ++c; });
+            cnt[i + 1] = c;
+        }
+    });
+    for (int i = 0; i < m; ++i) cnt[i + 1] += cnt[i];
+    SMFV_REQUIRE(cnt[m] <= 0x7fffffff, "fem27 nnz exceeds int32");
+    int *rp = xmalloc<int>((size_t)m + 1);
+    int *ci = xmalloc<int>((size_t)cnt[m]);
+    double *va = xmalloc<double>((size_t)cnt[m]);
+    if (!rp || !ci || !va) {
+        std::free(rp);
+        std::free(ci);
+        std::free(va);
+        set_error("out of memory");
+        return SMFV_ERR_HOST;
+    }
+    for (int i = 0; i <= m; ++i) rp[i] = (int)cnt[i];
+    parallel_rows(0, m, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            int64_t o = cnt[i];
+            visit(i, [&](int64_t j, double v) {
+                ci[o] = (int)j;
+                va[o] = v;
+                ++o;
+            });
+        }
+    });
+    *out_nnz = cnt[m];
+    *out_rp = rp;
+    *out_ci = ci;
+    *out_va = va;
+    return SMFV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// random rows: truncated power-law (alpha > 1) or fixed length (alpha <= 0)
+// ---------------------------------------------------------------------------
+static double powerlaw_raw(uint64_t seed, int64_t row, double alpha)
+{
+    // Pareto(x_m = 1): P(L >= x) = x^(1 - alpha)
+    const double u = 1.0 - u01(hash3(seed, (uint64_t)row, 0x5EEDull));  // (0, 1]
+    return std::pow(u, -1.0 / (alpha - 1.0));
+}
+
+static int64_t row_len(uint64_t seed, int64_t row, double alpha, double scale, int cap, int64_t n)
+{
+    int64_t L;
+    if (alpha <= 0) L = (int64_t)std::llround(scale);
+    else L = (int64_t)std::floor(powerlaw_raw(seed, row, alpha) * scale);
+    L = std::max<int64_t>(1, std::min<int64_t>(L, cap));
+    return std::min<int64_t>(L, n);
+}
+
+SMFV_API int smfv_gen_random_rows(int64_t m, int64_t n, int64_t row_begin, int64_t row_end,
+                                  double mean, double alpha, int cap, uint64_t seed,
+                                  int64_t *out_nnz, int **out_rp, int **out_ci, double **out_va)
+{
+    SMFV_REQUIRE(m >= 0 && n > 0 && 0 <= row_begin && row_begin <= row_end && row_end <= m,
+                 "bad row range");
+    SMFV_REQUIRE(mean >= 1 && cap >= 1 && (alpha <= 0 || alpha > 1), "bad distribution");
+    SMFV_REQUIRE(out_nnz && out_rp && out_ci && out_va, "null argument");
+    double scale = mean;
+    if (alpha > 0) {
+        // scale so that E[row length] == mean, estimated on a fixed sample of
+        // 2^16 hashed rows (independent of m and of the block): bisection
+        double lo = 0.01, hi = 4.0 * mean;
+        for (int it = 0; it < 60; ++it) {
+            const double mid = 0.5 * (lo + hi);
+            double s = 0;
+            for (int64_t r = 0; r < (1 << 16); ++r) s += (double)row_len(seed, r, alpha, mid, cap, n);
+            if (s / (1 << 16) < mean) lo = mid;
+            else hi = mid;
+        }
+        scale = 0.5 * (lo + hi);
+    }
+    const int64_t nr = row_end - row_begin;
+    std::vector<int64_t> cnt((size_t)nr + 1, 0);
+    parallel_rows(0, nr, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) cnt[i + 1] = row_len(seed, row_begin + i, alpha, scale, cap, n);
+    });
+    for (int64_t i = 0; i < nr; ++i) cnt[i + 1] += cnt[i];
+    SMFV_REQUIRE(cnt[nr] <= 0x7fffffff, "block nnz exceeds int32 row_ptr");
+    int *rp = xmalloc<int>((size_t)nr + 1);
+    int *ci = xmalloc<int>((size_t)cnt[nr]);
+    double *va = xmalloc<double>((size_t)cnt[nr]);
+    if (!rp || !ci || !va) {
+        std::free(rp);
+        std::free(ci);
+        std::free(va);
+        set_error("out of memory");
+        return SMFV_ERR_HOST;
+    }
+    for (int64_t i = 0; i <= nr; ++i) rp[i] = (int)cnt[i];
+    parallel_rows(0, nr, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            const int64_t row = row_begin + i;
+            int *c = ci + cnt[i];
+            const int64_t L = cnt[i + 1] - cnt[i];
+            for (int64_t k = 0; k < L; ++k)
+                c[k] = (int)(hash3(seed ^ 0xC0FFEEull, (uint64_t)row, (uint64_t)k) % (uint64_t)n);
+            std::sort(c, c + L);
+            for (int64_t k = 1; k < L; ++k)  // make distinct: bump forward ...
+                if (c[k] <= c[k - 1]) c[k] = c[k - 1] + 1;
+            for (int64_t k = L - 1; k >= 0; --k) {  // ... and pull back below n
+                const int64_t lim = n - (L - k);
+                if (c[k] > lim) c[k] = (int)lim;
+                else break;
+            }
+            for (int64_t k = 1; k < L; ++k)
+                if (c[k] <= c[k - 1]) c[k] = c[k - 1] + 1;
+            double *v = va + cnt[i];
+            for (int64_t k = 0; k < L; ++k)
+                v[k] = 2.0 * u01(hash3(seed ^ 0xBEEFull, (uint64_t)row, (uint64_t)k)) - 1.0;
+        }
+    });
+    *out_nnz = cnt[nr];
+    *out_rp = rp;
+    *out_ci = ci;
+    *out_va = va;
+    return SMFV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,47 @@
+// smfv_internal.h -- shared helpers of libsmfv (error state, checks).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "smfv.h"
+
+namespace smfv {
+
+void set_error(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+
+#define SMFV_REQUIRE(cond, ...)                   \
+    do {                                          \
+        if (!(cond)) {                            \
+            ::smfv::set_error(__VA_ARGS__);       \
+            return SMFV_ERR_INVALID;              \
+        }                                         \
+    } while (0)
+
+#define SMFV_HIP(call)                                                               \
+    do {                                                                             \
+        hipError_t e_ = (call);                                                      \
+        if (e_ != hipSuccess) {                                                      \
+            ::smfv::set_error("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), \
+                              __FILE__, __LINE__);                                   \
+            return SMFV_ERR_HIP;                                                     \
+        }                                                                            \
+    } while (0)
+
+// launch-error check after a <<<>>> launch
+#define SMFV_LAUNCHED() SMFV_HIP(hipGetLastError())
+
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// merge-path geometry shared by the kernels and the workspace query
+struct MergeGeom {
+    int64_t items;   // rows + nnz
+    int64_t ipt;     // merge-path items per team
+    int64_t nteams;
+};
+MergeGeom merge_geom(int nrows, int64_t nnz, int K);
+size_t merge_workspace_bytes(int nrows, int64_t nnz, int K);
+
+}  // namespace smfv

@@ -1,0 +1,724 @@
+// smfv_kernels.hip -- CDNA4 (gfx950) kernels of the CSR x fat-vector SpMM
+// hot path and the single-device C ABI (include/smfv.h).
+//
+// Reference loops replaced (SC = /root/reference/Source Code):
+//   k_rows   <- SC/SparseMatrixFatVectorMultiply.cpp:17-27 (sequential) and
+//               SC/SparseMatrixFatVectorMultiplyRowWise.cpp:36-50 (row block)
+//   k_rows with a column window (colpanel)
+//            <- SC/SparseMatrixFatVectorMultiplyColumnWise.cpp:34-48
+//   k_merge + k_carry_fixup
+//            <- SC/SparseMatrixFatVectorMultiplyNonZeroElement.cpp:24-67 (nnz
+//               partition) + :88 (sum of partial rows)
+//   k_panels_to_rowmajor <- SC/...ColumnWise.cpp:109-126 (rank-0 rebuild)
+//   k_combine_blocks     <- SC/...NonZeroElement.cpp:88 (MPI_Reduce SUM)
+//   k_compare            <- SC/utils.cpp:38-63 (areMatricesEqual)
+//
+// Layout: X[n x K] and Y[m x K] row-major (SC/utils.cpp:216-228 serialize),
+// CSR int32/f64 as SC/MatrixDefinitions.h:14-19.
+//
+// Thread mapping ("row team"): a team of TEAM lanes owns one CSR row; lane t
+// of the team owns VEC consecutive doubles of the output row (VEC = 2 ->
+// 16-byte loads/stores; a K = 32 row of X is one 256-byte, 2-cache-line
+// read by a 16-lane team).  The team reads TEAM (col, val) pairs with one
+// coalesced load and broadcasts them inside the team with ds_bpermute, so
+// each non-zero costs one 16-B/lane X gather.  Non-zeros of a row are
+// accumulated strictly in CSR order with a separate multiply and add (fp
+// contraction is off for this file), which makes SEQUENTIAL / ROWWISE /
+// COLUMNWISE bit-identical to the reference's x86-64 loop.
+//
+// Workgroups are remapped XCD-major (bijective): blocks dealt round-robin to
+// the 8 XCDs receive contiguous row ranges, so the X rows a band of the
+// matrix touches stay in one XCD's L2.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdarg>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "smfv_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace smfv {
+
+static thread_local std::string g_last_error;
+
+void set_error(const char *fmt, ...)
+{
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+}
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int xcd_remap(int b, int nwg)
+{
+    // blocks b, b+8, ... share an XCD; give each such group a contiguous
+    // range of logical block ids (bijective for any nwg; guide T1).
+    const int x = b & 7, q = nwg >> 3, r = nwg & 7;
+    const int base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    return base + (b >> 3);
+}
+
+template <int VEC> struct VecT;
+template <> struct VecT<1> {
+    using T = double;
+    __device__ static T load(const double *p) { return *p; }
+    __device__ static void store(double *p, T v) { *p = v; }
+    __device__ static T zero() { return 0.0; }
+    __device__ static T madd(T acc, double v, T x)
+    {
+        double p = v * x;
+        return acc + p;
+    }
+};
+template <> struct VecT<2> {
+    using T = double2;
+    __device__ static T load(const double *p) { return *reinterpret_cast<const double2 *>(p); }
+    __device__ static void store(double *p, T v) { *reinterpret_cast<double2 *>(p) = v; }
+    __device__ static T zero() { return make_double2(0.0, 0.0); }
+    __device__ static T madd(T acc, double v, T x)
+    {
+        double px = v * x.x, py = v * x.y;
+        return make_double2(acc.x + px, acc.y + py);
+    }
+};
+
+// Accumulate nnz [js, je) of one row into acc (team-uniform control flow).
+// X is indexed at column offset c (this lane's VEC columns); cok = lane owns
+// a valid column.  Strict CSR order, separate multiply/add.
+template <int TEAM, int VEC>
+__device__ __forceinline__ typename VecT<VEC>::T
+row_segment(int js, int je, const int *__restrict__ ci, const double *__restrict__ va,
+            const double *__restrict__ X, int64_t ldx, int c, bool cok,
+            typename VecT<VEC>::T acc)
+{
+    using V = VecT<VEC>;
+    if constexpr (TEAM == 1) {
+        int j = js;
+        for (; j + 4 <= je; j += 4) {
+            int c0 = ci[j], c1 = ci[j + 1], c2 = ci[j + 2], c3 = ci[j + 3];
+            double v0 = va[j], v1 = va[j + 1], v2 = va[j + 2], v3 = va[j + 3];
+            typename V::T x0 = V::zero(), x1 = V::zero(), x2 = V::zero(), x3 = V::zero();
+            if (cok) {
+                x0 = V::load(X + (int64_t)c0 * ldx + c);
+                x1 = V::load(X + (int64_t)c1 * ldx + c);
+                x2 = V::load(X + (int64_t)c2 * ldx + c);
+                x3 = V::load(X + (int64_t)c3 * ldx + c);
+            }
+            acc = V::madd(acc, v0, x0);
+            acc = V::madd(acc, v1, x1);
+            acc = V::madd(acc, v2, x2);
+            acc = V::madd(acc, v3, x3);
+        }
+        for (; j < je; ++j) {
+            const int cc = ci[j];
+            const double vv = va[j];
+            typename V::T x = V::zero();
+            if (cok) x = V::load(X + (int64_t)cc * ldx + c);
+            acc = V::madd(acc, vv, x);
+        }
+        return acc;
+    } else {
+        constexpr int U = TEAM < 8 ? TEAM : 8;
+        const int lane = threadIdx.x & 63;
+        const int tl = lane & (TEAM - 1);
+        const int tbase = lane & ~(TEAM - 1);
+        for (int j0 = js; j0 < je; j0 += TEAM) {
+            const int n = min(TEAM, je - j0);
+            int myc = 0;
+            double myv = 0.0;
+            if (tl < n) {
+                myc = ci[j0 + tl];
+                myv = va[j0 + tl];
+            }
+            for (int t0 = 0; t0 < n; t0 += U) {
+                int cc[U];
+                double vv[U];
+                typename V::T x[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int src = tbase + min(t0 + u, TEAM - 1);
+                    cc[u] = __shfl(myc, src);
+                    vv[u] = __shfl(myv, src);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    x[u] = V::zero();
+                    if (cok && t0 + u < n) x[u] = V::load(X + (int64_t)cc[u] * ldx + c);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (t0 + u < n) acc = V::madd(acc, vv[u], x[u]);
+            }
+        }
+        return acc;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_rows: rows [row_begin, row_begin + nrows) of Y (written at Y + lrow*ldy),
+// columns [0, K) of the (possibly offset) X.
+// ---------------------------------------------------------------------------
+template <int TEAM, int VEC>
+__global__ __launch_bounds__(256) void k_rows(int row_begin, int nrows, const int *__restrict__ rp,
+                                              const int *__restrict__ ci,
+                                              const double *__restrict__ va,
+                                              const double *__restrict__ X, int64_t ldx, int K,
+                                              double *__restrict__ Y, int64_t ldy)
+{
+    using V = VecT<VEC>;
+    constexpr int RPB = 256 / TEAM;  // rows per block
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int lrow = blk * RPB + (int)(threadIdx.x / TEAM);
+    if (lrow >= nrows) return;  // whole team leaves together
+    const int tl = threadIdx.x & (TEAM - 1);
+    const int row = row_begin + lrow;
+    const int js = rp[row], je = rp[row + 1];
+    double *yrow = Y + (int64_t)lrow * ldy;
+    const int npass = (K + TEAM * VEC - 1) / (TEAM * VEC);
+    for (int p = 0; p < npass; ++p) {
+        const int c = p * TEAM * VEC + tl * VEC;
+        const bool cok = c < K;
+        typename V::T acc = row_segment<TEAM, VEC>(js, je, ci, va, X, ldx, c, cok, V::zero());
+        if (cok) V::store(yrow + c, acc);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_merge: nnz-balanced merge-path over the rows [row_first, row_first +
+// nrows) restricted to nnz [s, e).  The merge list is {row ends} x {nnz};
+// team t walks diagonals [t*ipt, (t+1)*ipt).  Rows whose end falls in the
+// team's range are stored (possibly missing a prefix carried by earlier
+// teams); the row still open at the range end is written to the team's
+// carry slot, summed in team order by k_carry_fixup.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t merge_row_end(const int *rp, int row_first, int i, int64_t s,
+                                                 int64_t e)
+{
+    int64_t v = rp[row_first + i + 1];
+    return (v < e ? v : e) - s;
+}
+
+// number of rows i in [0, nrows) whose end event lies before diagonal d,
+// i.e. end(i) + i < d (end(i) + i is strictly increasing in i)
+__device__ __forceinline__ int merge_search(const int *rp, int row_first, int nrows, int64_t s,
+                                            int64_t e, int64_t d)
+{
+    int lo = 0, hi = nrows;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (merge_row_end(rp, row_first, mid, s, e) + mid < d) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+template <int TEAM, int VEC>
+__global__ __launch_bounds__(256) void k_merge(int row_first, int nrows, int64_t s, int64_t e,
+                                               const int *__restrict__ rp,
+                                               const int *__restrict__ ci,
+                                               const double *__restrict__ va,
+                                               const double *__restrict__ X, int64_t ldx, int K,
+                                               double *__restrict__ Yc, int64_t ldy, int64_t ipt,
+                                               int64_t nteams, int *__restrict__ carry_row,
+                                               double *__restrict__ carry_val)
+{
+    using V = VecT<VEC>;
+    constexpr int TPB = 256 / TEAM;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t t = (int64_t)blk * TPB + (threadIdx.x / TEAM);
+    if (t >= nteams) return;
+    const int tl = threadIdx.x & (TEAM - 1);
+    const int64_t total = (int64_t)nrows + (e - s);
+    const int64_t d0 = t * ipt;
+    const int64_t d1 = d0 + ipt < total ? d0 + ipt : total;
+    const int i0 = merge_search(rp, row_first, nrows, s, e, d0);
+    const int i1 = merge_search(rp, row_first, nrows, s, e, d1);
+    const int64_t j0 = d0 - i0, j1 = d1 - i1;  // relative nnz positions
+    bool carried = false;
+    const int npass = (K + TEAM * VEC - 1) / (TEAM * VEC);
+    for (int p = 0; p < npass; ++p) {
+        const int c = p * TEAM * VEC + tl * VEC;
+        const bool cok = c < K;
+        for (int i = i0; i <= i1 && i < nrows; ++i) {
+            const int64_t rs0 = rp[row_first + i];
+            const int64_t rs = (rs0 > s ? rs0 : s) - s;
+            const int64_t js = rs > j0 ? rs : j0;
+            const int64_t je = i < i1 ? merge_row_end(rp, row_first, i, s, e) : j1;
+            if (i == i1 && je <= js) break;  // nothing open at the range end
+            typename V::T acc = row_segment<TEAM, VEC>((int)(js + s), (int)(je + s), ci, va, X,
+                                                       ldx, c, cok, V::zero());
+            if (i < i1) {
+                if (cok) V::store(Yc + (int64_t)i * ldy + c, acc);
+            } else {
+                carried = true;
+                if (cok) V::store(carry_val + t * K + c, acc);
+            }
+        }
+    }
+    if (tl == 0) carry_row[t] = carried ? i1 : -1;
+}
+
+// one thread per (team, column): the first team of each run of equal carry
+// rows sums the run in team order and adds it to the stored row.
+__global__ __launch_bounds__(256) void k_carry_fixup(int64_t nteams, int K,
+                                                     const int *__restrict__ carry_row,
+                                                     const double *__restrict__ carry_val,
+                                                     double *__restrict__ Yc, int64_t ldy)
+{
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t t = g / K;
+    const int k = (int)(g - t * K);
+    if (t >= nteams) return;
+    const int r = carry_row[t];
+    if (r < 0) return;
+    if (t > 0 && carry_row[t - 1] == r) return;  // not the head of its run
+    double sum = carry_val[t * K + k];
+    for (int64_t u = t + 1; u < nteams && carry_row[u] == r; ++u) sum = sum + carry_val[u * K + k];
+    double *y = Yc + (int64_t)r * ldy + k;
+    *y = *y + sum;
+}
+
+// rank-major column panels -> row-major Y (SC/...ColumnWise.cpp:109-126)
+__global__ __launch_bounds__(256) void k_panels_to_rowmajor(int m, int K, int p,
+                                                            const double *__restrict__ panels,
+                                                            double *__restrict__ Y, int64_t ldy)
+{
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (int64_t)m * K) return;
+    const int64_t row = g / K;
+    const int col = (int)(g - row * K);
+    const int q = K / p;
+    int r = q > 0 ? col / q : p - 1;
+    if (r > p - 1) r = p - 1;
+    const int c0 = r * q;
+    const int kc = (r == p - 1) ? q + K % p : q;
+    const int64_t off = (int64_t)m * c0;  // ranks before r hold q columns each
+    Y[row * ldy + col] = panels[off + row * kc + (col - c0)];
+}
+
+struct BlockTable {
+    int p;
+    int rf[64];
+    int rl[64];
+    int64_t off[64];
+};
+
+// Y[row] = sum over ranks (in rank order) of their partial for row
+__global__ __launch_bounds__(256) void k_combine_blocks(int m, int K, BlockTable tab,
+                                                        const double *__restrict__ blocks,
+                                                        double *__restrict__ Y, int64_t ldy)
+{
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (int64_t)m * K) return;
+    const int row = (int)(g / K);
+    const int k = (int)(g - (int64_t)row * K);
+    double acc = 0.0;
+    bool any = false;
+    for (int r = 0; r < tab.p; ++r) {
+        if (row >= tab.rf[r] && row <= tab.rl[r]) {
+            const double v = blocks[tab.off[r] + (int64_t)(row - tab.rf[r]) * K + k];
+            acc = any ? acc + v : v;
+            any = true;
+        }
+    }
+    Y[(int64_t)row * ldy + k] = acc;
+}
+
+// max |a-b| and max |a-b| / max(|b|, 1e-300) as order-preserving u64 bit
+// patterns of non-negative doubles
+__global__ __launch_bounds__(256) void k_compare(int m, int K, const double *__restrict__ A,
+                                                 int64_t lda, const double *__restrict__ B,
+                                                 int64_t ldb, unsigned long long *out)
+{
+    __shared__ double s_abs[256], s_rel[256];
+    double mabs = 0.0, mrel = 0.0;
+    const int64_t total = (int64_t)m * K;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t row = g / K;
+        const int k = (int)(g - row * K);
+        const double a = A[row * lda + k], b = B[row * ldb + k];
+        double d = fabs(a - b);
+        if (d != d) d = INFINITY;
+        const double den = fabs(b) > 1e-300 ? fabs(b) : 1e-300;
+        mabs = fmax(mabs, d);
+        mrel = fmax(mrel, d / den);
+    }
+    s_abs[threadIdx.x] = mabs;
+    s_rel[threadIdx.x] = mrel;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            s_abs[threadIdx.x] = fmax(s_abs[threadIdx.x], s_abs[threadIdx.x + w]);
+            s_rel[threadIdx.x] = fmax(s_rel[threadIdx.x], s_rel[threadIdx.x + w]);
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        atomicMax(out, (unsigned long long)__double_as_longlong(s_abs[0]));
+        atomicMax(out + 1, (unsigned long long)__double_as_longlong(s_rel[0]));
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z)
+{
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_fill_x_hash(int64_t n, int K, uint64_t seed, double *X,
+                                                     int64_t ldx)
+{
+    const int64_t total = n * K;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = g / K;
+        const int k = (int)(g - i * K);
+        X[i * ldx + k] = (double)(1 + splitmix64(seed ^ (uint64_t)g) % 100);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host-side dispatch
+// ---------------------------------------------------------------------------
+static bool aligned16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+static int pick_vec(const double *X, int64_t ldx, const double *Y, int64_t ldy, int K)
+{
+    return (K % 2 == 0 && ldx % 2 == 0 && ldy % 2 == 0 && aligned16(X) && aligned16(Y)) ? 2 : 1;
+}
+
+static int pick_team(int K, int vec)
+{
+    int need = (K + vec - 1) / vec;
+    int t = 1;
+    while (t < need && t < 64) t <<= 1;
+    return t;
+}
+
+#define SMFV_TEAM_SWITCH(team, vec, LAUNCH)                 \
+    switch ((team) * 4 + (vec)) {                           \
+    case 1 * 4 + 1: LAUNCH(1, 1); break;                    \
+    case 1 * 4 + 2: LAUNCH(1, 2); break;                    \
+    case 2 * 4 + 1: LAUNCH(2, 1); break;                    \
+    case 2 * 4 + 2: LAUNCH(2, 2); break;                    \
+    case 4 * 4 + 1: LAUNCH(4, 1); break;                    \
+    case 4 * 4 + 2: LAUNCH(4, 2); break;                    \
+    case 8 * 4 + 1: LAUNCH(8, 1); break;                    \
+    case 8 * 4 + 2: LAUNCH(8, 2); break;                    \
+    case 16 * 4 + 1: LAUNCH(16, 1); break;                  \
+    case 16 * 4 + 2: LAUNCH(16, 2); break;                  \
+    case 32 * 4 + 1: LAUNCH(32, 1); break;                  \
+    case 32 * 4 + 2: LAUNCH(32, 2); break;                  \
+    case 64 * 4 + 1: LAUNCH(64, 1); break;                  \
+    case 64 * 4 + 2: LAUNCH(64, 2); break;                  \
+    default: set_error("internal: team %d vec %d", (team), (vec)); return SMFV_ERR_INVALID; \
+    }
+
+static int launch_rows(int row_begin, int nrows, const int *rp, const int *ci, const double *va,
+                       const double *X, int64_t ldx, int K, double *Y, int64_t ldy,
+                       hipStream_t st)
+{
+    if (nrows <= 0 || K <= 0) return SMFV_OK;
+    const int vec = pick_vec(X, ldx, Y, ldy, K);
+    const int team = pick_team(K, vec);
+    const int rpb = 256 / team;
+    const int64_t nblk = ((int64_t)nrows + rpb - 1) / rpb;
+    SMFV_REQUIRE(nblk <= 0x7fffffff, "too many rows for one launch");
+#define L(T_, V_) hipLaunchKernelGGL((k_rows<T_, V_>), dim3((unsigned)nblk), dim3(256), 0, st, \
+                                     row_begin, nrows, rp, ci, va, X, ldx, K, Y, ldy)
+    SMFV_TEAM_SWITCH(team, vec, L)
+#undef L
+    SMFV_LAUNCHED();
+    return SMFV_OK;
+}
+
+MergeGeom merge_geom(int nrows, int64_t nnz, int K)
+{
+    MergeGeom g;
+    g.items = (int64_t)nrows + nnz;
+    // ~64 teams per CU on 256 CUs, at least 32 items per team
+    const int64_t target = 256 * 64;
+    g.ipt = (g.items + target - 1) / target;
+    if (g.ipt < 32) g.ipt = 32;
+    (void)K;
+    g.nteams = g.items > 0 ? (g.items + g.ipt - 1) / g.ipt : 0;
+    return g;
+}
+
+size_t merge_workspace_bytes(int nrows, int64_t nnz, int K)
+{
+    const MergeGeom g = merge_geom(nrows, nnz, K);
+    const size_t rows_b = ((size_t)g.nteams * sizeof(int) + 255) & ~(size_t)255;
+    return rows_b + (size_t)g.nteams * (size_t)K * sizeof(double);
+}
+
+static int launch_merge(int row_first, int nrows, int64_t s, int64_t e, const int *rp,
+                        const int *ci, const double *va, const double *X, int64_t ldx, int K,
+                        double *Yc, int64_t ldy, void *ws, size_t ws_bytes, hipStream_t st)
+{
+    if (nrows <= 0 || K <= 0) return SMFV_OK;
+    const MergeGeom g = merge_geom(nrows, e - s, K);
+    const size_t need = merge_workspace_bytes(nrows, e - s, K);
+    SMFV_REQUIRE(ws != nullptr || need == 0, "NONZERO variant needs %zu bytes of workspace", need);
+    if (ws_bytes < need) {
+        set_error("workspace too small: %zu < %zu bytes", ws_bytes, need);
+        return SMFV_ERR_WORKSPACE;
+    }
+    SMFV_REQUIRE(aligned16(ws), "workspace must be 16-byte aligned");
+    int *carry_row = static_cast<int *>(ws);
+    const size_t rows_b = ((size_t)g.nteams * sizeof(int) + 255) & ~(size_t)255;
+    double *carry_val = reinterpret_cast<double *>(static_cast<char *>(ws) + rows_b);
+    const int vec = pick_vec(X, ldx, Yc, ldy, K);
+    const int team = pick_team(K, vec);
+    const int tpb = 256 / team;
+    const int64_t nblk = (g.nteams + tpb - 1) / tpb;
+    SMFV_REQUIRE(nblk <= 0x7fffffff, "too many merge teams for one launch");
+#define L(T_, V_) hipLaunchKernelGGL((k_merge<T_, V_>), dim3((unsigned)nblk), dim3(256), 0, st, \
+                                     row_first, nrows, s, e, rp, ci, va, X, ldx, K, Yc, ldy,    \
+                                     g.ipt, g.nteams, carry_row, carry_val)
+    SMFV_TEAM_SWITCH(team, vec, L)
+#undef L
+    SMFV_LAUNCHED();
+    const int64_t nthr = g.nteams * (int64_t)K;
+    const int64_t fblk = (nthr + 255) / 256;
+    SMFV_REQUIRE(fblk <= 0x7fffffff, "too many carry slots for one launch");
+    hipLaunchKernelGGL(k_carry_fixup, dim3((unsigned)fblk), dim3(256), 0, st, g.nteams, K,
+                       carry_row, carry_val, Yc, ldy);
+    SMFV_LAUNCHED();
+    return SMFV_OK;
+}
+
+}  // namespace smfv
+
+using namespace smfv;
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+SMFV_API const char *smfv_last_error(void) { return g_last_error.c_str(); }
+
+SMFV_API const char *smfv_version(void) { return "smfv 0.1.0 gfx950"; }
+
+SMFV_API void smfv_partition_rows(int m, int p, int r, int *start, int *end)
+{
+    const int q = m / p, extra = m % p;
+    const int s = r * q + (r < extra ? r : extra);
+    *start = s;
+    *end = s + q + (r < extra ? 1 : 0);
+}
+
+SMFV_API void smfv_partition_cols(int K, int p, int r, int *start, int *end)
+{
+    const int q = K / p, extra = K % p;
+    *start = r * q;
+    *end = (r != p - 1) ? r * q + q : r * q + q + extra;
+}
+
+SMFV_API void smfv_partition_nnz(int64_t nnz, int p, int r, int64_t *start, int64_t *end)
+{
+    const int64_t q = nnz / p, extra = nnz % p;
+    if (r < extra) {
+        *start = (int64_t)r * (q + 1);
+        *end = *start + q + 1;
+    } else {
+        *start = (int64_t)r * q + extra;
+        *end = *start + q;
+    }
+}
+
+SMFV_API int smfv_spmm_workspace_bytes(int variant, int m, int64_t nnz, int K, size_t *bytes)
+{
+    SMFV_REQUIRE(bytes != nullptr, "bytes is NULL");
+    SMFV_REQUIRE(m >= 0 && nnz >= 0 && K >= 0, "negative size");
+    SMFV_REQUIRE(variant >= SMFV_SEQUENTIAL && variant <= SMFV_NONZERO, "unknown variant %d", variant);
+    *bytes = variant == SMFV_NONZERO ? merge_workspace_bytes(m, nnz, K) : 0;
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz, const int *d_row_ptr,
+                               const int *d_col_idx, const double *d_values, const double *d_X,
+                               int64_t ldx, int K, double *d_Y, int64_t ldy, void *d_workspace,
+                               size_t workspace_bytes, void *stream)
+{
+    SMFV_REQUIRE(variant >= SMFV_SEQUENTIAL && variant <= SMFV_NONZERO, "unknown variant %d", variant);
+    SMFV_REQUIRE(m >= 0 && n >= 0 && nnz >= 0 && K >= 0, "negative size (m=%d n=%d nnz=%lld K=%d)",
+                 m, n, (long long)nnz, K);
+    SMFV_REQUIRE(nnz <= 0x7fffffff, "nnz %lld exceeds int32 row_ptr", (long long)nnz);
+    SMFV_REQUIRE(ldx >= K && ldy >= K, "leading dimension smaller than K");
+    if (m == 0 || K == 0) return SMFV_OK;
+    SMFV_REQUIRE(d_row_ptr && d_Y, "null row_ptr / Y");
+    SMFV_REQUIRE(nnz == 0 || (d_col_idx && d_values && d_X), "null col_idx / values / X");
+    hipStream_t st = as_stream(stream);
+    switch (variant) {
+    case SMFV_SEQUENTIAL:
+    case SMFV_ROWWISE:
+        return launch_rows(0, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, K, d_Y, ldy, st);
+    case SMFV_COLUMNWISE: {
+        // column panels of 8 doubles (64 B per row segment), one launch per
+        // panel group; same per-(row, column) summation as the reference.
+        const int kc = 8;
+        for (int c0 = 0; c0 < K; c0 += kc) {
+            const int w = std::min(kc, K - c0);
+            int rc = launch_rows(0, m, d_row_ptr, d_col_idx, d_values, d_X + c0, ldx, w, d_Y + c0,
+                                 ldy, st);
+            if (rc) return rc;
+        }
+        return SMFV_OK;
+    }
+    case SMFV_NONZERO:
+        return launch_merge(0, m, 0, nnz, d_row_ptr, d_col_idx, d_values, d_X, ldx, K, d_Y, ldy,
+                            d_workspace, workspace_bytes, st);
+    }
+    return SMFV_ERR_INVALID;
+}
+
+SMFV_API int smfv_spmm_rowblock_f64(int row_begin, int row_end, const int *d_row_ptr,
+                                    const int *d_col_idx, const double *d_values,
+                                    const double *d_X, int64_t ldx, int K, double *d_Yblock,
+                                    int64_t ldy, void *stream)
+{
+    SMFV_REQUIRE(row_begin >= 0 && row_end >= row_begin && K >= 0, "bad row block [%d, %d)",
+                 row_begin, row_end);
+    SMFV_REQUIRE(ldx >= K && ldy >= K, "leading dimension smaller than K");
+    return launch_rows(row_begin, row_end - row_begin, d_row_ptr, d_col_idx, d_values, d_X, ldx, K,
+                       d_Yblock, ldy, as_stream(stream));
+}
+
+SMFV_API int smfv_spmm_colpanel_f64(int m, int col_begin, int col_end, const int *d_row_ptr,
+                                    const int *d_col_idx, const double *d_values,
+                                    const double *d_X, int64_t ldx, double *d_panel, int64_t ldp,
+                                    void *stream)
+{
+    const int kc = col_end - col_begin;
+    SMFV_REQUIRE(m >= 0 && col_begin >= 0 && kc >= 0 && col_end <= ldx, "bad column panel");
+    SMFV_REQUIRE(ldp >= kc, "panel leading dimension smaller than panel width");
+    return launch_rows(0, m, d_row_ptr, d_col_idx, d_values, d_X + col_begin, ldx, kc, d_panel, ldp,
+                       as_stream(stream));
+}
+
+SMFV_API int smfv_nnz_range_rows(int m, const int *h_row_ptr, int64_t nnz_begin, int64_t nnz_end,
+                                 int *row_first, int *row_last)
+{
+    SMFV_REQUIRE(h_row_ptr && row_first && row_last, "null argument");
+    SMFV_REQUIRE(0 <= nnz_begin && nnz_begin <= nnz_end && nnz_end <= h_row_ptr[m],
+                 "bad nnz range");
+    if (nnz_begin == nnz_end) {
+        *row_first = 0;
+        *row_last = -1;
+        return SMFV_OK;
+    }
+    // row containing nnz_begin: last i with row_ptr[i] <= nnz_begin and row non-empty
+    const int *b = h_row_ptr, *e = h_row_ptr + m + 1;
+    const int rf = (int)(std::upper_bound(b, e, (int)nnz_begin) - b) - 1;
+    const int rl = (int)(std::upper_bound(b, e, (int)(nnz_end - 1)) - b) - 1;
+    *row_first = rf;
+    *row_last = rl;
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_spmm_nnzrange_workspace_bytes(int nrows, int64_t nnz_count, int K, size_t *bytes)
+{
+    SMFV_REQUIRE(bytes && nrows >= 0 && nnz_count >= 0 && K >= 0, "bad argument");
+    *bytes = merge_workspace_bytes(nrows, nnz_count, K);
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_spmm_nnzrange_f64(int row_first, int row_last, int64_t nnz_begin,
+                                    int64_t nnz_end, const int *d_row_ptr, const int *d_col_idx,
+                                    const double *d_values, const double *d_X, int64_t ldx, int K,
+                                    double *d_Ypart, int64_t ldy, void *d_workspace,
+                                    size_t workspace_bytes, void *stream)
+{
+    SMFV_REQUIRE(nnz_begin >= 0 && nnz_end >= nnz_begin && K >= 0, "bad nnz range");
+    SMFV_REQUIRE(ldx >= K && ldy >= K, "leading dimension smaller than K");
+    const int nrows = row_last - row_first + 1;
+    if (nrows <= 0) return SMFV_OK;
+    return launch_merge(row_first, nrows, nnz_begin, nnz_end, d_row_ptr, d_col_idx, d_values, d_X,
+                        ldx, K, d_Ypart, ldy, d_workspace, workspace_bytes, as_stream(stream));
+}
+
+SMFV_API int smfv_panels_to_rowmajor_f64(int m, int K, int p, const double *d_panels, double *d_Y,
+                                         int64_t ldy, void *stream)
+{
+    SMFV_REQUIRE(m >= 0 && K >= 0 && p > 0 && ldy >= K, "bad argument");
+    const int64_t total = (int64_t)m * K;
+    if (total == 0) return SMFV_OK;
+    const int64_t nblk = (total + 255) / 256;
+    SMFV_REQUIRE(nblk <= 0x7fffffff, "too large");
+    hipLaunchKernelGGL(k_panels_to_rowmajor, dim3((unsigned)nblk), dim3(256), 0, as_stream(stream),
+                       m, K, p, d_panels, d_Y, ldy);
+    SMFV_LAUNCHED();
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_combine_row_blocks_f64(int m, int K, int p, const int *h_row_first,
+                                         const int *h_row_last, const double *d_blocks,
+                                         double *d_Y, int64_t ldy, void *stream)
+{
+    SMFV_REQUIRE(m >= 0 && K >= 0 && p > 0 && p <= 64 && ldy >= K, "bad argument (p <= 64)");
+    BlockTable tab;
+    std::memset(&tab, 0, sizeof tab);
+    tab.p = p;
+    int64_t off = 0;
+    for (int r = 0; r < p; ++r) {
+        tab.rf[r] = h_row_first[r];
+        tab.rl[r] = h_row_last[r];
+        tab.off[r] = off;
+        const int nr = h_row_last[r] - h_row_first[r] + 1;
+        if (nr > 0) off += (int64_t)nr * K;
+    }
+    const int64_t total = (int64_t)m * K;
+    if (total == 0) return SMFV_OK;
+    const int64_t nblk = (total + 255) / 256;
+    SMFV_REQUIRE(nblk <= 0x7fffffff, "too large");
+    hipLaunchKernelGGL(k_combine_blocks, dim3((unsigned)nblk), dim3(256), 0, as_stream(stream), m,
+                       K, tab, d_blocks, d_Y, ldy);
+    SMFV_LAUNCHED();
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_compare_f64(int m, int K, const double *d_A, int64_t lda, const double *d_B,
+                              int64_t ldb, double *h_out, void *stream)
+{
+    SMFV_REQUIRE(h_out && m >= 0 && K >= 0 && lda >= K && ldb >= K, "bad argument");
+    hipStream_t st = as_stream(stream);
+    unsigned long long *d_out = nullptr;
+    SMFV_HIP(hipMallocAsync(reinterpret_cast<void **>(&d_out), 2 * sizeof(unsigned long long), st));
+    SMFV_HIP(hipMemsetAsync(d_out, 0, 2 * sizeof(unsigned long long), st));
+    if ((int64_t)m * K > 0)
+        hipLaunchKernelGGL(k_compare, dim3(1024), dim3(256), 0, st, m, K, d_A, lda, d_B, ldb, d_out);
+    SMFV_LAUNCHED();
+    unsigned long long h[2] = {0, 0};
+    SMFV_HIP(hipMemcpyAsync(h, d_out, sizeof h, hipMemcpyDeviceToHost, st));
+    SMFV_HIP(hipFreeAsync(d_out, st));
+    SMFV_HIP(hipStreamSynchronize(st));
+    std::memcpy(h_out, h, sizeof h);
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_fill_x_hash_f64(int64_t n, int K, uint64_t seed, double *d_X, int64_t ldx,
+                                  void *stream)
+{
+    SMFV_REQUIRE(n >= 0 && K >= 0 && ldx >= K && (n == 0 || K == 0 || d_X), "bad argument");
+    if (n * K == 0) return SMFV_OK;
+    hipLaunchKernelGGL(k_fill_x_hash, dim3(4096), dim3(256), 0, as_stream(stream), n, K, seed, d_X,
+                       ldx);
+    SMFV_LAUNCHED();
+    return SMFV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,222 @@
+"""Device-side SpMM: Y = A_csr * X on an MI355X through the libsmfv C ABI.
+
+Python mirror of the reference's hot-path call surface
+(SC = /root/reference/Source Code):
+
+    sparseMatrixFatVectorMultiply              SC/SparseMatrixFatVectorMultiply.h:14-15
+    sparseMatrixFatVectorMultiplyRowWise       SC/SparseMatrixFatVectorMultiplyRowWise.h:15-17
+    sparseMatrixFatVectorMultiplyColumnWise    SC/SparseMatrixFatVectorMultiplyColumnWise.h:15
+    sparseMatrixFatVectorMultiplyNonZeroElement SC/SparseMatrixFatVectorMultiplyNonZeroElement.h:15
+
+Same arguments (A, fat vector, vecCols) and result (m x K, row-major).  The
+MPI variants are collective over a Communicator (dist.py) when one is given
+and return the result on rank 0 only (an empty (0, K) array elsewhere), as
+SC/...RowWise.cpp:125 does; without one they run on the local GPU.
+
+torch is used only for device memory and the current HIP stream.  Every
+compute call goes to the HIP kernels; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_size_t
+from enum import IntEnum
+
+import numpy as np
+import torch
+
+from ._lib import call
+from .inputs import SparseMatrix
+
+
+class Variant(IntEnum):
+    SEQUENTIAL = 0   # SC/SparseMatrixFatVectorMultiply.cpp:11-31
+    ROWWISE = 1      # SC/SparseMatrixFatVectorMultiplyRowWise.cpp:12-126
+    COLUMNWISE = 2   # SC/SparseMatrixFatVectorMultiplyColumnWise.cpp:13-131
+    NONZERO = 3      # SC/SparseMatrixFatVectorMultiplyNonZeroElement.cpp:12-120
+
+
+def _require_device() -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("smfv: no HIP device visible; the SpMM engine has no CPU path")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def stream_handle(stream: torch.cuda.Stream | None = None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+class DeviceCSR:
+    """A CSR matrix resident in HBM (int32 row_ptr / col_idx, f64 values)
+    plus the host copy of row_ptr the nnz partitioning needs."""
+
+    def __init__(self, A: SparseMatrix, device: torch.device | None = None):
+        device = device or _require_device()
+        A.validate()
+        self.m, self.n, self.nnz = A.numRows, A.numCols, A.nnz
+        self.h_row_ptr = np.ascontiguousarray(A.rowPtr, dtype=np.int32)
+        self.row_ptr = torch.from_numpy(self.h_row_ptr).to(device)
+        self.col_idx = torch.from_numpy(np.ascontiguousarray(A.colIndices, dtype=np.int32)).to(device)
+        self.values = torch.from_numpy(np.ascontiguousarray(A.values, dtype=np.float64)).to(device)
+        self.device = device
+
+    @property
+    def nbytes(self) -> int:
+        return 4 * (self.m + 1) + 12 * self.nnz
+
+    def ptrs(self):
+        return self.row_ptr.data_ptr(), self.col_idx.data_ptr(), self.values.data_ptr()
+
+
+def workspace_bytes(variant: int, m: int, nnz: int, K: int) -> int:
+    b = c_size_t(0)
+    call("smfv_spmm_workspace_bytes", int(variant), m, nnz, K, byref(b))
+    return b.value
+
+
+def _check_dense(T: torch.Tensor, rows: int, K: int, name: str) -> int:
+    if not T.is_cuda or T.dtype != torch.float64:
+        raise TypeError(f"{name} must be a float64 HIP tensor")
+    if T.dim() != 2 or T.shape[0] != rows or T.shape[1] != K:
+        raise ValueError(f"{name} must have shape ({rows}, {K}), got {tuple(T.shape)}")
+    if K > 0 and T.stride(1) != 1:
+        raise ValueError(f"{name} must be row-major (unit column stride)")
+    return max(int(T.stride(0)), K)
+
+
+class SpmmPlan:
+    """Pre-sized execution of one variant for (A, K): the workspace is
+    allocated once so run() is a pure asynchronous launch sequence
+    (capturable into a hipGraph)."""
+
+    def __init__(self, variant: int, A: DeviceCSR, K: int):
+        self.variant, self.A, self.K = Variant(variant), A, K
+        nb = workspace_bytes(variant, A.m, A.nnz, K)
+        self.workspace = torch.empty(max(nb, 1), dtype=torch.uint8, device=A.device) if nb else None
+        self.ws_bytes = nb
+
+    def run(self, X: torch.Tensor, Y: torch.Tensor, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+        A, K = self.A, self.K
+        ldx = _check_dense(X, A.n, K, "X")
+        ldy = _check_dense(Y, A.m, K, "Y")
+        rp, ci, va = A.ptrs()
+        ws = self.workspace.data_ptr() if self.workspace is not None else None
+        call("smfv_spmm_csr_f64", int(self.variant), A.m, A.n, A.nnz, rp, ci, va, X.data_ptr(), ldx,
+             K, Y.data_ptr(), ldy, ws, self.ws_bytes, stream_handle(stream))
+        return Y
+
+
+def spmm(variant: int, A: DeviceCSR, X: torch.Tensor, Y: torch.Tensor | None = None,
+         stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """Y = A * X on the device (asynchronous on `stream`)."""
+    K = X.shape[1]
+    if Y is None:
+        Y = torch.empty((A.m, K), dtype=torch.float64, device=A.device)
+    return SpmmPlan(variant, A, K).run(X, Y, stream)
+
+
+def spmm_rowblock(A: DeviceCSR, row_begin: int, row_end: int, X: torch.Tensor, Yblock: torch.Tensor,
+                  stream=None) -> torch.Tensor:
+    K = X.shape[1]
+    ldx = _check_dense(X, A.n, K, "X")
+    ldy = _check_dense(Yblock, row_end - row_begin, K, "Yblock")
+    rp, ci, va = A.ptrs()
+    call("smfv_spmm_rowblock_f64", row_begin, row_end, rp, ci, va, X.data_ptr(), ldx, K,
+         Yblock.data_ptr(), ldy, stream_handle(stream))
+    return Yblock
+
+
+def spmm_colpanel(A: DeviceCSR, col_begin: int, col_end: int, X: torch.Tensor, panel: torch.Tensor,
+                  stream=None) -> torch.Tensor:
+    K = X.shape[1]
+    ldx = _check_dense(X, A.n, K, "X")
+    ldp = _check_dense(panel, A.m, col_end - col_begin, "panel")
+    rp, ci, va = A.ptrs()
+    call("smfv_spmm_colpanel_f64", A.m, col_begin, col_end, rp, ci, va, X.data_ptr(), ldx,
+         panel.data_ptr(), max(ldp, 1), stream_handle(stream))
+    return panel
+
+
+def nnz_range_rows(A_host_row_ptr: np.ndarray, nnz_begin: int, nnz_end: int) -> tuple[int, int]:
+    rp = np.ascontiguousarray(A_host_row_ptr, dtype=np.int32)
+    rf, rl = ctypes.c_int(0), ctypes.c_int(0)
+    call("smfv_nnz_range_rows", len(rp) - 1, rp.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+         nnz_begin, nnz_end, byref(rf), byref(rl))
+    return rf.value, rl.value
+
+
+def spmm_nnzrange(A: DeviceCSR, nnz_begin: int, nnz_end: int, X: torch.Tensor, stream=None):
+    """Partial rows of the nnz range (SC/...NonZeroElement.cpp:56-67):
+    returns (row_first, row_last, Ypart[(row_last-row_first+1) x K])."""
+    K = X.shape[1]
+    ldx = _check_dense(X, A.n, K, "X")
+    rf, rl = nnz_range_rows(A.h_row_ptr, nnz_begin, nnz_end)
+    nr = max(0, rl - rf + 1)
+    Yp = torch.empty((nr, K), dtype=torch.float64, device=A.device)
+    b = c_size_t(0)
+    call("smfv_spmm_nnzrange_workspace_bytes", nr, nnz_end - nnz_begin, K, byref(b))
+    ws = torch.empty(max(b.value, 1), dtype=torch.uint8, device=A.device)
+    rp, ci, va = A.ptrs()
+    call("smfv_spmm_nnzrange_f64", rf, rl, nnz_begin, nnz_end, rp, ci, va, X.data_ptr(), ldx, K,
+         Yp.data_ptr(), max(K, 1), ws.data_ptr(), b.value, stream_handle(stream))
+    return rf, rl, Yp
+
+
+def compare(A: torch.Tensor, B: torch.Tensor, stream=None) -> tuple[float, float]:
+    """Device areMatricesEqual (SC/utils.cpp:38-63): (max abs diff, max rel diff)."""
+    m, K = A.shape
+    lda = _check_dense(A, m, K, "A")
+    ldb = _check_dense(B, m, K, "B")
+    out = (ctypes.c_double * 2)()
+    call("smfv_compare_f64", m, K, A.data_ptr(), lda, B.data_ptr(), ldb, out, stream_handle(stream))
+    return out[0], out[1]
+
+
+def fill_x_hash(X: torch.Tensor, seed: int, stream=None) -> torch.Tensor:
+    n, K = X.shape
+    ldx = _check_dense(X, n, K, "X")
+    call("smfv_fill_x_hash_f64", n, K, seed, X.data_ptr(), ldx, stream_handle(stream))
+    return X
+
+
+# ---------------------------------------------------------------------------
+# the reference's four functions (host arrays in, host array out)
+# ---------------------------------------------------------------------------
+def _run_host(variant: Variant, A: SparseMatrix, fatVector, vecCols: int) -> np.ndarray:
+    X = np.ascontiguousarray(np.asarray(fatVector, dtype=np.float64).reshape(A.numCols, vecCols))
+    dA = DeviceCSR(A)
+    dX = torch.from_numpy(X).to(dA.device)
+    Y = spmm(variant, dA, dX)
+    return Y.cpu().numpy()
+
+
+def sparseMatrixFatVectorMultiply(sparseMatrix: SparseMatrix, fatVector, vecCols: int) -> np.ndarray:
+    return _run_host(Variant.SEQUENTIAL, sparseMatrix, fatVector, vecCols)
+
+
+def _collective(variant: Variant, A: SparseMatrix, fatVector, vecCols: int, comm) -> np.ndarray:
+    if comm is None or comm.size == 1:
+        return _run_host(variant, A, fatVector, vecCols)
+    from .dist import dist_spmm
+    dA = DeviceCSR(A)
+    X = np.ascontiguousarray(np.asarray(fatVector, dtype=np.float64).reshape(A.numCols, vecCols))
+    dX = torch.from_numpy(X).to(dA.device)
+    Y = dist_spmm(comm, variant, dA, dX, to_all=False, root=0)
+    torch.cuda.synchronize()
+    return Y.cpu().numpy() if comm.rank == 0 else np.empty((0, vecCols))
+
+
+def sparseMatrixFatVectorMultiplyRowWise(sparseMatrix: SparseMatrix, fatVector, vecCols: int,
+                                         comm=None) -> np.ndarray:
+    return _collective(Variant.ROWWISE, sparseMatrix, fatVector, vecCols, comm)
+
+
+def sparseMatrixFatVectorMultiplyColumnWise(sparseMatrix: SparseMatrix, fatVector, vecCols: int,
+                                            comm=None) -> np.ndarray:
+    return _collective(Variant.COLUMNWISE, sparseMatrix, fatVector, vecCols, comm)
+
+
+def sparseMatrixFatVectorMultiplyNonZeroElement(sparseMatrix: SparseMatrix, fatVector, vecCols: int,
+                                                comm=None) -> np.ndarray:
+    return _collective(Variant.NONZERO, sparseMatrix, fatVector, vecCols, comm)
