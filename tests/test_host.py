@@ -1,0 +1,191 @@
+"""CPU-only tests of the product's host side: the C ABI library loads and
+exports every symbol the headers declare, partitions / plans / reader /
+fat-vector / generators agree with the oracle and the reference fixtures.
+No device calls here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, ROOT, golden_cases, load_golden
+from oracle import oracle
+
+import sparsematrixmultiplicationmpi_amd as smfv
+from sparsematrixmultiplicationmpi_amd import _lib, inputs
+from sparsematrixmultiplicationmpi_amd.dist import exchange_plan
+
+INCLUDE = os.path.join(ROOT, "include")
+PKG = os.path.join(ROOT, "sparsematrixmultiplicationmpi_amd")
+
+
+def header_symbols(header):
+    src = open(os.path.join(INCLUDE, header)).read()
+    return set(re.findall(r"SMFV_API\s+[\w\s\*]+?\b(smfv_\w+)\s*\(", src))
+
+
+def test_c_abi_exports_every_declared_symbol():
+    declared = header_symbols("smfv.h") | header_symbols("smfv_host.h")
+    assert len(declared) >= 30
+    nm = subprocess.run(["nm", "-D", "--defined-only", os.path.join(PKG, "libsmfv.so")],
+                        capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (smfv_\w+)", nm))
+    assert declared <= exported, declared - exported
+    # and the ctypes binding covers all of them
+    assert declared <= set(_lib.exported_symbols())
+    assert _lib.lib.smfv_version().decode().startswith("smfv")
+
+
+def test_dropin_library_exports_reference_surface():
+    nm = subprocess.run(["nm", "-DC", "--defined-only", os.path.join(PKG, "libsmfv_mpi.so")],
+                        capture_output=True, text=True, check=True).stdout
+    for sym in ("sparseMatrixFatVectorMultiply(SparseMatrix const&",
+                "sparseMatrixFatVectorMultiplyRowWise(SparseMatrix const&",
+                "sparseMatrixFatVectorMultiplyColumnWise(SparseMatrix const&",
+                "sparseMatrixFatVectorMultiplyNonZeroElement(SparseMatrix const&",
+                "readMatrixMarketFile(", "generateLargeFatVector(int, int)", "areMatricesEqual(",
+                "serialize(", "deserialize("):
+        assert sym in nm, sym
+    assert os.access(os.path.join(PKG, "smfv_main"), os.X_OK)
+
+
+def _part(fn, *args):
+    a, b = (ctypes.c_int64(), ctypes.c_int64()) if fn == "smfv_partition_nnz" else (ctypes.c_int(), ctypes.c_int())
+    getattr(_lib.lib, fn)(*args, ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+def test_partitions_equal_oracle():
+    for m in (0, 1, 3, 8, 100, 121192):
+        for p in (1, 2, 3, 7, 8, 64):
+            for r in range(p):
+                assert _part("smfv_partition_rows", m, p, r) == oracle.partition_rows(m, p, r)
+                assert _part("smfv_partition_cols", m, p, r) == oracle.partition_cols(m, p, r)
+                assert _part("smfv_partition_nnz", m * 7, p, r) == oracle.partition_nnz(m * 7, p, r)
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("p", [1, 2, 3, 8, 13])
+def test_exchange_plan_covers_output(variant, p):
+    A = smfv.gen_random_rows(700, 500, 6, 2.0, 200, 5)
+    # add empty rows at both ends and in the middle
+    lens = np.diff(A.rowPtr)
+    lens[[0, 1, 350, 699]] = 0
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    K = 5
+    first, last, off, cnt = exchange_plan(variant, 700, int(rp[-1]), rp, K, p)
+    if variant == 1:   # rows tile [0, m)
+        assert first[0] == 0 and last[-1] == 699
+        assert np.all(first[1:] == last[:-1] + 1)
+        assert np.all(off == first * K) and np.all(cnt == (last - first + 1) * K)
+    elif variant == 2:  # columns tile [0, K), panels back to back
+        assert first[0] == 0 and last[-1] == K - 1
+        assert np.all(off == 700 * first)
+        assert cnt.sum() == 700 * K
+    else:              # nnz ranges: touched rows, consecutive compact blocks
+        nnz = int(rp[-1])
+        for r in range(p):
+            s, e = oracle.partition_nnz(nnz, p, r)
+            if e > s:
+                assert rp[first[r]] <= s < rp[first[r] + 1]
+                assert rp[last[r]] <= e - 1 < rp[last[r] + 1]
+            else:
+                assert cnt[r] == 0
+        assert np.all(off[1:] == off[:-1] + cnt[:-1])
+        # every non-empty row is covered by some rank
+        covered = np.zeros(700, bool)
+        for r in range(p):
+            covered[first[r]:last[r] + 1] = True
+        assert np.all(covered[lens > 0])
+
+
+def test_host_reader_matches_oracle_and_golden():
+    for f in ("sym5.mtx", "pat4x6.mtx", "empty7x5.mtx"):
+        A = smfv.readMatrixMarketFile(os.path.join(GOLDEN, f))
+        m, n, rp, ci, va = oracle.mtx_read(os.path.join(GOLDEN, f))
+        assert (A.numRows, A.numCols) == (m, n)
+        assert np.array_equal(A.rowPtr, rp) and np.array_equal(A.colIndices, ci)
+        assert np.array_equal(A.values, va)
+
+
+def test_host_reader_roundtrip_and_errors(tmp_path):
+    A = smfv.gen_fem27(500, 8, 8, 0.8, 3)
+    p = tmp_path / "a.mtx"
+    smfv.writeMatrixMarketFile(str(p), A, symmetric=True)
+    B = smfv.readMatrixMarketFile(str(p))
+    assert np.array_equal(A.rowPtr, B.rowPtr) and np.array_equal(A.colIndices, B.colIndices)
+    assert np.array_equal(A.values, B.values)
+    m, n, rp, ci, va = oracle.mtx_read(str(p))
+    assert np.array_equal(rp, B.rowPtr) and np.array_equal(va, B.values)
+    with pytest.raises(smfv.SmfvError):
+        smfv.readMatrixMarketFile(str(tmp_path / "missing.mtx"))
+    bad = tmp_path / "bad.mtx"
+    bad.write_text("%%MatrixMarket matrix coordinate real general\n\n2 2 1\n1 1 1\n")
+    with pytest.raises(smfv.SmfvError):   # blank size line: UB in the reference, error here
+        smfv.readMatrixMarketFile(str(bad))
+
+
+def test_fatvector_matches_reference_rand():
+    for name, info in golden_cases().items():
+        if info["x"].startswith("glibc"):
+            g = load_golden(name)
+            assert np.array_equal(smfv.generateLargeFatVector(int(g["n"]), g["X"].shape[1]), g["X"])
+    X = smfv.generateLargeFatVector(3000, 7)
+    assert np.array_equal(X, oracle.fatvector_rand(3000, 7))
+
+
+def test_serialize_roundtrip():
+    fat = [[1.0, 2.0, 3.0], [4.0, 5.0, 6.0]]
+    flat = smfv.serialize(fat)
+    assert flat.tolist() == [1, 2, 3, 4, 5, 6]
+    assert smfv.deserialize(flat, 2, 3).tolist() == fat
+    assert smfv.areMatricesEqual(fat, [[1.0, 2.0, 3.0], [4.0, 5.0, 6.0 + 1e-7]], 1e-6)
+    assert not smfv.areMatricesEqual(fat, [[1.0, 2.0, 3.0], [4.0, 5.0, 6.1]], 1e-6)
+    assert not smfv.areMatricesEqual(fat, [[1.0, 2.0, 3.0]], 1e-6)
+
+
+def test_generators():
+    A = smfv.cop20k_surrogate()
+    A.validate()
+    assert A.numRows == smfv.COP20K_M and abs(A.nnz - smfv.COP20K_NNZ) < 100
+    # exactly symmetric
+    import scipy.sparse as sp
+    M = sp.csr_matrix((A.values, A.colIndices, A.rowPtr), shape=(A.numRows, A.numCols))
+    assert (M != M.T).nnz == 0
+    # sorted, distinct columns per row; deterministic
+    B = smfv.gen_random_rows(20000, 30000, 16, 2.0, 4096, 9)
+    B.validate()
+    d = np.diff(B.colIndices)
+    starts = B.rowPtr[1:-1]
+    mask = np.ones(len(d), bool)
+    mask[starts[starts < len(d) + 1] - 1] = False
+    assert np.all(d[mask] > 0)
+    C = smfv.gen_random_rows(20000, 30000, 16, 2.0, 4096, 9)
+    assert np.array_equal(B.colIndices, C.colIndices) and np.array_equal(B.values, C.values)
+    assert 14 < B.nnz / B.numRows < 18
+    # a row block equals the same rows of the whole matrix
+    blk = smfv.gen_random_rows(20000, 30000, 16, 2.0, 4096, 9, 5000, 6000)
+    assert np.array_equal(blk.colIndices, B.colIndices[B.rowPtr[5000]:B.rowPtr[6000]])
+    U = smfv.gen_random_rows(1000, 1000, 16, 0.0, 16, 1)
+    assert np.all(np.diff(U.rowPtr) == 16)
+
+
+def test_csr_bin_roundtrip(tmp_path):
+    A = smfv.gen_fem27(300, 7, 7, 0.7, 2)
+    p = str(tmp_path / "a.bin")
+    inputs.write_csr_bin(p, A)
+    B = inputs.read_csr_bin(p)
+    assert np.array_equal(A.rowPtr, B.rowPtr) and np.array_equal(A.values, B.values)
+
+
+def test_product_has_no_oracle_dependency():
+    """The product never imports, links or calls the oracle."""
+    for dirpath, _, files in os.walk(PKG):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h", "Makefile")):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in src.lower().replace("oracle_", ""), f
+    nm = subprocess.run(["nm", "-D", os.path.join(PKG, "libsmfv.so")], capture_output=True, text=True).stdout
+    assert "oracle_" not in nm
