@@ -15,7 +15,7 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
   ok $rc || exit $rc
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.log" 2>&1
   rc=$?; echo "smoke rc=$rc"; tail -n 5 "$OUT/smoke_$TAG.log"
-  [ $rc -eq 0 ] || exit $rc
+  ok $rc || exit $rc
 fi
 timeout -k 10 ${BENCH_TIMEOUT:-400} python bench.py ${BENCH_ARGS:-} > "$OUT/bench_$TAG.log" 2>&1
 rc=$?; echo "bench rc=$rc"; tail -c 4000 "$OUT/bench_$TAG.log"

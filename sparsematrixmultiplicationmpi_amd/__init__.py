@@ -22,7 +22,7 @@ from .inputs import (  # noqa: F401
     serialize,
     writeMatrixMarketFile,
 )
-from .spmm import (  # noqa: F401
+from .engine import (  # noqa: F401
     DeviceCSR,
     SpmmPlan,
     Variant,

@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from ._lib import call, lib
-from .spmm import DeviceCSR, Variant, stream_handle
+from .engine import DeviceCSR, Variant, stream_handle
 
 UNIQUE_ID_BYTES = 128
 TO_ROOT, TO_ALL = 0, 1

@@ -14,7 +14,7 @@ from conftest import golden_cases, load_golden
 from oracle import oracle
 
 import sparsematrixmultiplicationmpi_amd as smfv
-from sparsematrixmultiplicationmpi_amd import spmm as S
+from sparsematrixmultiplicationmpi_amd import engine as S
 
 pytestmark = pytest.mark.gpu
 NNZ_TOL = 1e-12
