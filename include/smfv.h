@@ -97,8 +97,9 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz,
 
 /* Rank-local building blocks of the distributed variants (also usable on
  * their own).  Row block [row_begin, row_end) of Y (row-major, ldy):
- * what one rank of SC/...RowWise.cpp:36-50 computes. */
-SMFV_API int smfv_spmm_rowblock_f64(int row_begin, int row_end, const int *d_row_ptr,
+ * what one rank of SC/...RowWise.cpp:36-50 computes.  n = rows of X (all
+ * rank-local functions take it: it bounds every X access). */
+SMFV_API int smfv_spmm_rowblock_f64(int row_begin, int row_end, int n, const int *d_row_ptr,
                                     const int *d_col_idx, const double *d_values,
                                     const double *d_X, int64_t ldx, int K,
                                     double *d_Yblock, int64_t ldy, void *stream);
@@ -106,7 +107,7 @@ SMFV_API int smfv_spmm_rowblock_f64(int row_begin, int row_end, const int *d_row
 /* Column panel [col_begin, col_end) of Y for all m rows, written as a
  * [m x (col_end-col_begin)] panel with leading dimension ldp: what one rank
  * of SC/...ColumnWise.cpp:34-48 computes. */
-SMFV_API int smfv_spmm_colpanel_f64(int m, int col_begin, int col_end, const int *d_row_ptr,
+SMFV_API int smfv_spmm_colpanel_f64(int m, int n, int col_begin, int col_end, const int *d_row_ptr,
                                     const int *d_col_idx, const double *d_values,
                                     const double *d_X, int64_t ldx,
                                     double *d_panel, int64_t ldp, void *stream);
@@ -119,7 +120,7 @@ SMFV_API int smfv_nnz_range_rows(int m, const int *h_row_ptr, int64_t nnz_begin,
                                  int *row_first, int *row_last);
 SMFV_API int smfv_spmm_nnzrange_workspace_bytes(int nrows, int64_t nnz_count, int K, size_t *bytes);
 SMFV_API int smfv_spmm_nnzrange_f64(int row_first, int row_last, int64_t nnz_begin, int64_t nnz_end,
-                                    const int *d_row_ptr, const int *d_col_idx,
+                                    int n, const int *d_row_ptr, const int *d_col_idx,
                                     const double *d_values, const double *d_X, int64_t ldx, int K,
                                     double *d_Ypart, int64_t ldy,
                                     void *d_workspace, size_t workspace_bytes, void *stream);

@@ -46,13 +46,13 @@ _SIGS = {
     "smfv_spmm_csr_f64": (c_int, [c_int, c_int, c_int, c_int64, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_int64, c_int, c_void_p, c_int64, c_void_p, c_size_t,
                                   c_void_p]),
-    "smfv_spmm_rowblock_f64": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+    "smfv_spmm_rowblock_f64": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_int64, c_int, c_void_p, c_int64, c_void_p]),
-    "smfv_spmm_colpanel_f64": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+    "smfv_spmm_colpanel_f64": (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_int64, c_void_p, c_int64, c_void_p]),
     "smfv_nnz_range_rows": (c_int, [c_int, _PI, c_int64, c_int64, _PI, _PI]),
     "smfv_spmm_nnzrange_workspace_bytes": (c_int, [c_int, c_int64, c_int, POINTER(c_size_t)]),
-    "smfv_spmm_nnzrange_f64": (c_int, [c_int, c_int, c_int64, c_int64, c_void_p, c_void_p,
+    "smfv_spmm_nnzrange_f64": (c_int, [c_int, c_int, c_int64, c_int64, c_int, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64,
                                        c_void_p, c_size_t, c_void_p]),
     "smfv_panels_to_rowmajor_f64": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_int64,

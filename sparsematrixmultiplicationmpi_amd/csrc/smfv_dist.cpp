@@ -224,12 +224,12 @@ SMFV_API int smfv_dist_spmm_f64(smfv_comm_t comm, int variant, int mode, int roo
     double *xbuf = nullptr;
     if (variant == SMFV_ROWWISE || variant == SMFV_SEQUENTIAL) {
         xbuf = d_Y;
-        rc = smfv_spmm_rowblock_f64(P.first[rank], P.last[rank] + 1, d_row_ptr, d_col_idx,
+        rc = smfv_spmm_rowblock_f64(P.first[rank], P.last[rank] + 1, n, d_row_ptr, d_col_idx,
                                     d_values, d_X, K, K, d_Y + P.offset[rank], K, stream);
     } else if (variant == SMFV_COLUMNWISE) {
         xbuf = static_cast<double *>(d_workspace);
         const int kc = P.last[rank] - P.first[rank] + 1;
-        rc = smfv_spmm_colpanel_f64(m, P.first[rank], P.last[rank] + 1, d_row_ptr, d_col_idx,
+        rc = smfv_spmm_colpanel_f64(m, n, P.first[rank], P.last[rank] + 1, d_row_ptr, d_col_idx,
                                     d_values, d_X, K, xbuf + P.offset[rank], std::max(1, kc),
                                     stream);
     } else if (variant == SMFV_NONZERO) {
@@ -237,7 +237,7 @@ SMFV_API int smfv_dist_spmm_f64(smfv_comm_t comm, int variant, int mode, int roo
         const size_t blocks_b = align256((size_t)P.total * sizeof(double));
         int64_t s, e;
         smfv_partition_nnz(nnz, p, rank, &s, &e);
-        rc = smfv_spmm_nnzrange_f64(P.first[rank], P.last[rank], s, e, d_row_ptr, d_col_idx,
+        rc = smfv_spmm_nnzrange_f64(P.first[rank], P.last[rank], s, e, n, d_row_ptr, d_col_idx,
                                     d_values, d_X, K, K, xbuf + P.offset[rank], K,
                                     static_cast<char *>(d_workspace) + blocks_b,
                                     workspace_bytes - blocks_b, stream);

@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -189,6 +190,135 @@ __global__ __launch_bounds__(256) void k_rows(int row_begin, int nrows, const in
         const bool cok = c < K;
         typename V::T acc = row_segment<TEAM, VEC>(js, je, ci, va, X, ldx, c, cok, V::zero());
         if (cok) V::store(yrow + c, acc);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_rows_mh: the production row kernel for K even and 16-byte aligned X/Y.
+//
+//  * a block of 256 lanes owns 256/TEAM consecutive rows; it stages its
+//    row_ptr slice and its non-zero range (col, val) into LDS with one
+//    coalesced pass (chunks of STAGE_CAP non-zeros if it holds more), so the
+//    dependent global round trips are row_ptr -> CSR -> X only;
+//  * a team of TEAM lanes owns one row; lane t holds H double2 column groups
+//    at columns 2t + 2*TEAM*h (h < H), i.e. each of the H 16-byte loads of a
+//    team reads one contiguous 32*TEAM-byte segment of the X row -- full
+//    coalescing while 64/TEAM rows share every per-non-zero instruction
+//    (LDS read of col/val, address arithmetic, loop control);
+//  * X is read through a buffer resource with a 32-bit byte offset
+//    (col * ldx * 8 + lane column) and the column-group step as the
+//    instruction's immediate offset (BUF = true, X < 4 GiB); BUF = false
+//    is the 64-bit pointer path for larger X;
+//  * U non-zeros' X rows are in flight per team before they are accumulated
+//    in CSR order (separate multiply and add: bit-identical to the
+//    reference's sequential loop).
+// ---------------------------------------------------------------------------
+constexpr int STAGE_CAP = 1024;  // non-zeros staged per block pass (12 KiB)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int TEAM, int H, int U, bool BUF>
+__global__ __launch_bounds__(256) void k_rows_mh(int row_begin, int nrows,
+                                                 const int *__restrict__ rp,
+                                                 const int *__restrict__ ci,
+                                                 const double *__restrict__ va,
+                                                 const double *__restrict__ X, int64_t ldx,
+                                                 uint32_t xbytes, int K, double *__restrict__ Y,
+                                                 int64_t ldy)
+{
+    constexpr int RPB = 256 / TEAM;
+    constexpr int CP = 2 * TEAM * H;  // columns per pass
+    constexpr int PER_THREAD = STAGE_CAP / 256;
+    __shared__ int s_rp[RPB + 1];
+    __shared__ int s_ci[STAGE_CAP];
+    __shared__ double s_va[STAGE_CAP];
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int row0 = blk * RPB;
+    const int nr = min(RPB, nrows - row0);
+    const int tid = threadIdx.x;
+    for (int i = tid; i <= nr; i += 256) s_rp[i] = rp[row_begin + row0 + i];  // nr + 1 entries
+    __syncthreads();
+    const int bs = s_rp[0], be = s_rp[nr];
+    const int team = tid / TEAM, tl = tid & (TEAM - 1);
+    const bool live = team < nr;
+    const int js = live ? s_rp[team] : 0, je = live ? s_rp[team + 1] : 0;
+    double *yrow = Y + (int64_t)(row0 + team) * ldy;
+    // (BUF = false never reads xr; the descriptor is then an empty range)
+    const __amdgpu_buffer_rsrc_t xr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)X, 0, BUF ? (int)xbytes : 0, 0x00020000);
+    const uint32_t ldxb = (uint32_t)(ldx * 8);
+    const int npass = (K + CP - 1) / CP;
+    for (int p = 0; p < npass; ++p) {
+        const int cb = p * CP + 2 * tl;  // this lane's first column in the pass
+        bool ok[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) ok[h] = cb + 2 * TEAM * h < K;
+        double2 acc[H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) acc[h] = make_double2(0.0, 0.0);
+        for (int c0 = bs; c0 < be; c0 += STAGE_CAP) {
+            const int cnt = min(STAGE_CAP, be - c0);
+            if (c0 != bs || p != 0) __syncthreads();  // previous chunk fully consumed
+            int rc[PER_THREAD];
+            double rv[PER_THREAD];
+#pragma unroll
+            for (int u = 0; u < PER_THREAD; ++u) {
+                const int idx = u * 256 + tid;
+                rc[u] = 0;
+                rv[u] = 0.0;
+                if (idx < cnt) {
+                    rc[u] = ci[c0 + idx];
+                    rv[u] = va[c0 + idx];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < PER_THREAD; ++u) {
+                const int idx = u * 256 + tid;
+                if (idx < cnt) {
+                    s_ci[idx] = rc[u];
+                    s_va[idx] = rv[u];
+                }
+            }
+            __syncthreads();
+            if (!live) continue;
+            const int a = max(js, c0) - c0, b = min(je, c0 + cnt) - c0;
+            for (int j0 = a; j0 < b; j0 += U) {
+                double2 x[U][H];
+                double vv[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    vv[u] = 0.0;
+#pragma unroll
+                    for (int h = 0; h < H; ++h) x[u][h] = make_double2(0.0, 0.0);
+                    if (j0 + u < b) {
+                        const int cc = s_ci[j0 + u];
+                        vv[u] = s_va[j0 + u];
+                        if constexpr (BUF) {
+                            const int off = (int)((uint32_t)cc * ldxb + (uint32_t)cb * 8u);
+#pragma unroll
+                            for (int h = 0; h < H; ++h)
+                                if (ok[h])
+                                    x[u][h] = __builtin_bit_cast(
+                                        double2, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     xr, off + h * 16 * TEAM, 0, 0));
+                        } else {
+                            const double *px = X + (int64_t)cc * ldx + cb;
+#pragma unroll
+                            for (int h = 0; h < H; ++h)
+                                if (ok[h]) x[u][h] = *reinterpret_cast<const double2 *>(px + 2 * TEAM * h);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (j0 + u < b)
+#pragma unroll
+                        for (int h = 0; h < H; ++h) acc[h] = VecT<2>::madd(acc[h], vv[u], x[u][h]);
+            }
+        }
+        if (live)
+#pragma unroll
+            for (int h = 0; h < H; ++h)
+                if (ok[h]) *reinterpret_cast<double2 *>(yrow + cb + 2 * TEAM * h) = acc[h];
     }
 }
 
@@ -426,19 +556,77 @@ static int pick_team(int K, int vec)
     default: set_error("internal: team %d vec %d", (team), (vec)); return SMFV_ERR_INVALID; \
     }
 
+// Row-kernel configuration (TEAM lanes per row, H column groups per lane,
+// U gathers in flight per team) by K; SMFV_ROW_CFG="TEAM,H,U" overrides it
+// for A/B measurement (only configurations instantiated below exist).
+struct RowCfg {
+    int team, h, u;
+};
+
+static RowCfg row_cfg_for(int K)
+{
+    static const char *env = std::getenv("SMFV_ROW_CFG");
+    if (env) {
+        RowCfg c{0, 0, 0};
+        if (std::sscanf(env, "%d,%d,%d", &c.team, &c.h, &c.u) == 3) return c;
+    }
+    const int pairs = K / 2;  // double2 columns
+    if (pairs >= 64) return {16, 4, 4};
+    if (pairs >= 16) return {8, 2, 8};
+    if (pairs >= 8) return {8, 1, 8};
+    if (pairs >= 4) return {4, 1, 8};
+    if (pairs >= 2) return {2, 1, 8};
+    return {1, 1, 8};
+}
+
+#define SMFV_MH_CONFIGS(X_) \
+    X_(1, 1, 8) X_(2, 1, 8) X_(4, 1, 8) X_(8, 1, 8) X_(16, 1, 8) X_(16, 1, 16) X_(8, 2, 4)    \
+    X_(8, 2, 8) X_(4, 4, 4) X_(4, 4, 2) X_(2, 8, 2) X_(16, 2, 4) X_(16, 4, 4) X_(32, 2, 4)   \
+    X_(64, 1, 8) X_(8, 8, 2) X_(16, 4, 2) X_(32, 1, 8)
+
+static int launch_rows_mh(int row_begin, int nrows, const int *rp, const int *ci, const double *va,
+                          const double *X, int64_t ldx, int64_t xrows, int K, double *Y,
+                          int64_t ldy, hipStream_t st)
+{
+    const RowCfg cfg = row_cfg_for(K);
+    const int rpb = 256 / cfg.team;
+    const int64_t nblk = ((int64_t)nrows + rpb - 1) / rpb;
+    SMFV_REQUIRE(nblk <= 0x7fffffff, "too many rows for one launch");
+    const int64_t xb = xrows * ldx * 8;
+    const bool buf = xb > 0 && xb <= 0x7fffffffLL;
+    const uint32_t xbytes = buf ? (uint32_t)xb : 0u;
+#define L(T_, H_, U_)                                                                               \
+    if (cfg.team == T_ && cfg.h == H_ && cfg.u == U_) {                                             \
+        if (buf)                                                                                    \
+            hipLaunchKernelGGL((k_rows_mh<T_, H_, U_, true>), dim3((unsigned)nblk), dim3(256), 0,   \
+                               st, row_begin, nrows, rp, ci, va, X, ldx, xbytes, K, Y, ldy);        \
+        else                                                                                        \
+            hipLaunchKernelGGL((k_rows_mh<T_, H_, U_, false>), dim3((unsigned)nblk), dim3(256), 0,  \
+                               st, row_begin, nrows, rp, ci, va, X, ldx, xbytes, K, Y, ldy);        \
+        SMFV_LAUNCHED();                                                                            \
+        return SMFV_OK;                                                                             \
+    }
+    SMFV_MH_CONFIGS(L)
+#undef L
+    set_error("row kernel configuration %d,%d,%d is not instantiated", cfg.team, cfg.h, cfg.u);
+    return SMFV_ERR_INVALID;
+}
+
 static int launch_rows(int row_begin, int nrows, const int *rp, const int *ci, const double *va,
-                       const double *X, int64_t ldx, int K, double *Y, int64_t ldy,
+                       const double *X, int64_t ldx, int64_t xrows, int K, double *Y, int64_t ldy,
                        hipStream_t st)
 {
     if (nrows <= 0 || K <= 0) return SMFV_OK;
     const int vec = pick_vec(X, ldx, Y, ldy, K);
-    const int team = pick_team(K, vec);
+    if (vec == 2) return launch_rows_mh(row_begin, nrows, rp, ci, va, X, ldx, xrows, K, Y, ldy, st);
+    // odd K or unaligned X / Y: one double per lane, shuffle-broadcast kernel
+    const int team = pick_team(K, 1);
     const int rpb = 256 / team;
     const int64_t nblk = ((int64_t)nrows + rpb - 1) / rpb;
     SMFV_REQUIRE(nblk <= 0x7fffffff, "too many rows for one launch");
 #define L(T_, V_) hipLaunchKernelGGL((k_rows<T_, V_>), dim3((unsigned)nblk), dim3(256), 0, st, \
                                      row_begin, nrows, rp, ci, va, X, ldx, K, Y, ldy)
-    SMFV_TEAM_SWITCH(team, vec, L)
+    SMFV_TEAM_SWITCH(team, 1, L)
 #undef L
     SMFV_LAUNCHED();
     return SMFV_OK;
@@ -566,14 +754,14 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz, const int
     switch (variant) {
     case SMFV_SEQUENTIAL:
     case SMFV_ROWWISE:
-        return launch_rows(0, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, K, d_Y, ldy, st);
+        return launch_rows(0, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, n, K, d_Y, ldy, st);
     case SMFV_COLUMNWISE: {
         // column panels of 8 doubles (64 B per row segment), one launch per
         // panel group; same per-(row, column) summation as the reference.
         const int kc = 8;
         for (int c0 = 0; c0 < K; c0 += kc) {
             const int w = std::min(kc, K - c0);
-            int rc = launch_rows(0, m, d_row_ptr, d_col_idx, d_values, d_X + c0, ldx, w, d_Y + c0,
+            int rc = launch_rows(0, m, d_row_ptr, d_col_idx, d_values, d_X + c0, ldx, n, w, d_Y + c0,
                                  ldy, st);
             if (rc) return rc;
         }
@@ -586,7 +774,7 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz, const int
     return SMFV_ERR_INVALID;
 }
 
-SMFV_API int smfv_spmm_rowblock_f64(int row_begin, int row_end, const int *d_row_ptr,
+SMFV_API int smfv_spmm_rowblock_f64(int row_begin, int row_end, int n, const int *d_row_ptr,
                                     const int *d_col_idx, const double *d_values,
                                     const double *d_X, int64_t ldx, int K, double *d_Yblock,
                                     int64_t ldy, void *stream)
@@ -594,11 +782,12 @@ SMFV_API int smfv_spmm_rowblock_f64(int row_begin, int row_end, const int *d_row
     SMFV_REQUIRE(row_begin >= 0 && row_end >= row_begin && K >= 0, "bad row block [%d, %d)",
                  row_begin, row_end);
     SMFV_REQUIRE(ldx >= K && ldy >= K, "leading dimension smaller than K");
-    return launch_rows(row_begin, row_end - row_begin, d_row_ptr, d_col_idx, d_values, d_X, ldx, K,
-                       d_Yblock, ldy, as_stream(stream));
+    SMFV_REQUIRE(n >= 0, "negative n");
+    return launch_rows(row_begin, row_end - row_begin, d_row_ptr, d_col_idx, d_values, d_X, ldx, n,
+                       K, d_Yblock, ldy, as_stream(stream));
 }
 
-SMFV_API int smfv_spmm_colpanel_f64(int m, int col_begin, int col_end, const int *d_row_ptr,
+SMFV_API int smfv_spmm_colpanel_f64(int m, int n, int col_begin, int col_end, const int *d_row_ptr,
                                     const int *d_col_idx, const double *d_values,
                                     const double *d_X, int64_t ldx, double *d_panel, int64_t ldp,
                                     void *stream)
@@ -606,8 +795,9 @@ SMFV_API int smfv_spmm_colpanel_f64(int m, int col_begin, int col_end, const int
     const int kc = col_end - col_begin;
     SMFV_REQUIRE(m >= 0 && col_begin >= 0 && kc >= 0 && col_end <= ldx, "bad column panel");
     SMFV_REQUIRE(ldp >= kc, "panel leading dimension smaller than panel width");
-    return launch_rows(0, m, d_row_ptr, d_col_idx, d_values, d_X + col_begin, ldx, kc, d_panel, ldp,
-                       as_stream(stream));
+    SMFV_REQUIRE(n >= 0, "negative n");
+    return launch_rows(0, m, d_row_ptr, d_col_idx, d_values, d_X + col_begin, ldx, n, kc, d_panel,
+                       ldp, as_stream(stream));
 }
 
 SMFV_API int smfv_nnz_range_rows(int m, const int *h_row_ptr, int64_t nnz_begin, int64_t nnz_end,
@@ -638,7 +828,7 @@ SMFV_API int smfv_spmm_nnzrange_workspace_bytes(int nrows, int64_t nnz_count, in
 }
 
 SMFV_API int smfv_spmm_nnzrange_f64(int row_first, int row_last, int64_t nnz_begin,
-                                    int64_t nnz_end, const int *d_row_ptr, const int *d_col_idx,
+                                    int64_t nnz_end, int n, const int *d_row_ptr, const int *d_col_idx,
                                     const double *d_values, const double *d_X, int64_t ldx, int K,
                                     double *d_Ypart, int64_t ldy, void *d_workspace,
                                     size_t workspace_bytes, void *stream)

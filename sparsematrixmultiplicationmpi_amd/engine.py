@@ -122,7 +122,7 @@ def spmm_rowblock(A: DeviceCSR, row_begin: int, row_end: int, X: torch.Tensor, Y
     ldx = _check_dense(X, A.n, K, "X")
     ldy = _check_dense(Yblock, row_end - row_begin, K, "Yblock")
     rp, ci, va = A.ptrs()
-    call("smfv_spmm_rowblock_f64", row_begin, row_end, rp, ci, va, X.data_ptr(), ldx, K,
+    call("smfv_spmm_rowblock_f64", row_begin, row_end, A.n, rp, ci, va, X.data_ptr(), ldx, K,
          Yblock.data_ptr(), ldy, stream_handle(stream))
     return Yblock
 
@@ -133,7 +133,7 @@ def spmm_colpanel(A: DeviceCSR, col_begin: int, col_end: int, X: torch.Tensor, p
     ldx = _check_dense(X, A.n, K, "X")
     ldp = _check_dense(panel, A.m, col_end - col_begin, "panel")
     rp, ci, va = A.ptrs()
-    call("smfv_spmm_colpanel_f64", A.m, col_begin, col_end, rp, ci, va, X.data_ptr(), ldx,
+    call("smfv_spmm_colpanel_f64", A.m, A.n, col_begin, col_end, rp, ci, va, X.data_ptr(), ldx,
          panel.data_ptr(), max(ldp, 1), stream_handle(stream))
     return panel
 
@@ -158,7 +158,7 @@ def spmm_nnzrange(A: DeviceCSR, nnz_begin: int, nnz_end: int, X: torch.Tensor, s
     call("smfv_spmm_nnzrange_workspace_bytes", nr, nnz_end - nnz_begin, K, byref(b))
     ws = torch.empty(max(b.value, 1), dtype=torch.uint8, device=A.device)
     rp, ci, va = A.ptrs()
-    call("smfv_spmm_nnzrange_f64", rf, rl, nnz_begin, nnz_end, rp, ci, va, X.data_ptr(), ldx, K,
+    call("smfv_spmm_nnzrange_f64", rf, rl, nnz_begin, nnz_end, A.n, rp, ci, va, X.data_ptr(), ldx, K,
          Yp.data_ptr(), max(K, 1), ws.data_ptr(), b.value, stream_handle(stream))
     return rf, rl, Yp
 
