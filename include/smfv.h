@@ -95,6 +95,31 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz,
                                double *d_Y, int64_t ldy,
                                void *d_workspace, size_t workspace_bytes, void *stream);
 
+/* ---- plans: analysed once per (matrix pattern, K), executed many times --
+ * The plan owns all device workspace (merge-path carries for NONZERO) and,
+ * for SEQUENTIAL / ROWWISE / COLUMNWISE with K a multiple of 32, a row-tile
+ * analysis of the pattern (h_col_idx needed): tiles of <= 16 consecutive
+ * rows whose distinct X rows fit a 32 KiB LDS image, with 16-bit local
+ * column indices.  The tiled kernel stages each tile's X rows once and reads
+ * them from LDS -- same per-row order and arithmetic, bit-identical result.
+ * Tiling is used when the measured re-use (non-zeros per staged X row) is
+ * >= 1.25 or SMFV_PLAN_FORCE_TILES is set.  Creation allocates device memory
+ * and synchronises; execution is asynchronous and graph-capturable.  The
+ * same d_row_ptr / d_col_idx / d_values the plan was built from must be
+ * passed to every execute (the plan does not copy A). */
+typedef struct smfv_plan_s *smfv_plan_t;
+#define SMFV_PLAN_NO_TILES 1
+#define SMFV_PLAN_FORCE_TILES 2
+SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
+                              const int *h_row_ptr, const int *h_col_idx, int K, int flags);
+SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int *d_col_idx,
+                               const double *d_values, const double *d_X, int64_t ldx,
+                               double *d_Y, int64_t ldy, void *stream);
+/* out[0] tiled (0/1), [1] tiles, [2] staged X rows per panel, [3] re-use
+ * (tiled non-zeros / staged rows), [4] plan device bytes, [5] direct tiles */
+SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[6]);
+SMFV_API int smfv_plan_destroy(smfv_plan_t plan);
+
 /* Rank-local building blocks of the distributed variants (also usable on
  * their own).  Row block [row_begin, row_end) of Y (row-major, ldy):
  * what one rank of SC/...RowWise.cpp:36-50 computes.  n = rows of X (all

@@ -46,6 +46,12 @@ _SIGS = {
     "smfv_spmm_csr_f64": (c_int, [c_int, c_int, c_int, c_int64, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_int64, c_int, c_void_p, c_int64, c_void_p, c_size_t,
                                   c_void_p]),
+    "smfv_plan_create": (c_int, [POINTER(c_void_p), c_int, c_int, c_int, c_int64, _PI, _PI, c_int,
+                                 c_int]),
+    "smfv_plan_execute": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                  c_void_p, c_int64, c_void_p]),
+    "smfv_plan_stats": (c_int, [c_void_p, _PD]),
+    "smfv_plan_destroy": (c_int, [c_void_p]),
     "smfv_spmm_rowblock_f64": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_int64, c_int, c_void_p, c_int64, c_void_p]),
     "smfv_spmm_colpanel_f64": (c_int, [c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,

@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "smfv_internal.h"
+#include "smfv_plan.h"
 
 #pragma clang fp contract(off)
 
@@ -320,6 +321,81 @@ __global__ __launch_bounds__(256) void k_rows_mh(int row_begin, int nrows,
             for (int h = 0; h < H; ++h)
                 if (ok[h]) *reinterpret_cast<double2 *>(yrow + cb + 2 * TEAM * h) = acc[h];
     }
+}
+
+// ---------------------------------------------------------------------------
+// k_rows_tiled: one workgroup per row tile (consecutive rows, see
+// smfv_plan.cpp) and per 32-column panel of X / Y.
+//   1. the tile's distinct X rows (panel slice, 256 B each) are copied into
+//      LDS with LDS-DMA (global_load_lds_dwordx4: one wave-instruction moves
+//      4 rows = 1 KiB, lane-linear into a dense [u][32] image);
+//   2. a 16-lane team per row walks the row's non-zeros in CSR order: lane t
+//      holds (local column, value) of 16 consecutive non-zeros, broadcasts
+//      them inside the team (ds_bpermute) and reads the 16-byte X slice with
+//      one conflict-free ds_read_b128 (a 256-B row covers the 64 banks).
+// The X rows a tile re-uses are fetched from L2/HBM once instead of once per
+// non-zero; tiles whose union does not fit (one row wider than TILE_UCAP)
+// gather X directly.  Same per-row order and arithmetic as the reference.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_rows_tiled(
+    const int *__restrict__ tile_rows, const int *__restrict__ tile_uoff,
+    const uint8_t *__restrict__ tile_direct, const int *__restrict__ ucols,
+    const uint16_t *__restrict__ lidx, const int *__restrict__ rp, const int *__restrict__ ci,
+    const double *__restrict__ va, const double *__restrict__ X, int64_t ldx, int K,
+    double *__restrict__ Y, int64_t ldy)
+{
+    __shared__ __attribute__((aligned(16))) double s_x[TILE_UCAP * TILE_KP];
+    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int cp = blockIdx.y * TILE_KP;  // first column of this panel
+    const int r0 = tile_rows[t], r1 = tile_rows[t + 1];
+    const int u0 = tile_uoff[t], nu = tile_uoff[t + 1] - u0;
+    const bool direct = tile_direct[t] != 0;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tl = tid & 15, tbase = lane & ~15;
+    if (!direct) {
+        for (int g = wave; g * 4 < nu; g += 4) {
+            const int u = min(g * 4 + (lane >> 4), nu - 1);  // pad lanes re-read a valid row
+            const double *src = X + (int64_t)ucols[u0 + u] * ldx + cp + 2 * tl;
+            __builtin_amdgcn_global_load_lds(
+                (const void *)src, (__attribute__((address_space(3))) void *)(s_x + g * 128), 16, 0, 0);
+        }
+    }
+    __syncthreads();  // drains the LDS-DMA (vmcnt(0)) and publishes the image
+    const int row = r0 + (tid >> 4);
+    if (row >= r1) return;
+    const int js = rp[row], je = rp[row + 1];
+    double2 acc = make_double2(0.0, 0.0);
+    if (!direct) {
+        constexpr int U = 8;
+        const double2 *sx = reinterpret_cast<const double2 *>(s_x) + tl;
+        for (int j0 = js; j0 < je; j0 += 16) {
+            const int n = min(16, je - j0);
+            int my_l = 0;
+            double my_v = 0.0;
+            if (tl < n) {
+                my_l = lidx[j0 + tl];
+                my_v = va[j0 + tl];
+            }
+            for (int t0 = 0; t0 < n; t0 += U) {
+                double2 x[U];
+                double v[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int src = tbase + min(t0 + u, 15);
+                    const int l = __shfl(my_l, src);
+                    v[u] = __shfl(my_v, src);
+                    x[u] = make_double2(0.0, 0.0);
+                    if (t0 + u < n) x[u] = sx[l * (TILE_KP / 2)];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (t0 + u < n) acc = VecT<2>::madd(acc, v[u], x[u]);
+            }
+        }
+    } else {
+        acc = row_segment<16, 2>(js, je, ci, va, X, ldx, cp + 2 * tl, true, acc);
+    }
+    if (cp + 2 * tl < K) *reinterpret_cast<double2 *>(Y + (int64_t)row * ldy + cp + 2 * tl) = acc;
 }
 
 // ---------------------------------------------------------------------------
@@ -772,6 +848,133 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz, const int
                             d_workspace, workspace_bytes, st);
     }
     return SMFV_ERR_INVALID;
+}
+
+// ---- plans (analysed once per matrix pattern and K) ------------------------
+}  // extern "C"
+
+struct smfv_plan_s {
+    int variant = 0, m = 0, n = 0, K = 0;
+    int64_t nnz = 0;
+    bool tiled = false;
+    int ntiles = 0, ndirect = 0;
+    int64_t union_rows = 0, tiled_nnz = 0;
+    int *tile_rows = nullptr, *tile_uoff = nullptr, *ucols = nullptr;
+    uint8_t *tile_direct = nullptr;
+    uint16_t *lidx = nullptr;
+    void *ws = nullptr;
+    size_t ws_bytes = 0, dev_bytes = 0;
+    ~smfv_plan_s()
+    {
+        for (void *q : {(void *)tile_rows, (void *)tile_uoff, (void *)ucols, (void *)tile_direct,
+                        (void *)lidx, ws})
+            if (q) (void)hipFree(q);
+    }
+};
+
+namespace {
+template <class T> int upload(T **dst, const std::vector<T> &src, size_t &acc)
+{
+    const size_t b = std::max<size_t>(src.size(), 1) * sizeof(T);
+    SMFV_HIP(hipMalloc(reinterpret_cast<void **>(dst), b));
+    if (!src.empty()) SMFV_HIP(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    acc += b;
+    return SMFV_OK;
+}
+}  // namespace
+
+extern "C" {
+
+SMFV_API int smfv_plan_create(smfv_plan_t *out, int variant, int m, int n, int64_t nnz,
+                              const int *h_row_ptr, const int *h_col_idx, int K, int flags)
+{
+    SMFV_REQUIRE(out, "null plan pointer");
+    SMFV_REQUIRE(variant >= SMFV_SEQUENTIAL && variant <= SMFV_NONZERO, "unknown variant %d", variant);
+    SMFV_REQUIRE(m >= 0 && n >= 0 && nnz >= 0 && nnz <= 0x7fffffff && K >= 0, "bad sizes");
+    SMFV_REQUIRE(h_row_ptr == nullptr || h_row_ptr[m] == nnz, "row_ptr[m] != nnz");
+    auto *p = new smfv_plan_s;
+    p->variant = variant;
+    p->m = m;
+    p->n = n;
+    p->K = K;
+    p->nnz = nnz;
+    int rc = SMFV_OK;
+    if (variant == SMFV_NONZERO) {
+        p->ws_bytes = merge_workspace_bytes(m, nnz, K);
+        if (p->ws_bytes) {
+            hipError_t e = hipMalloc(&p->ws, p->ws_bytes);
+            if (e != hipSuccess) {
+                set_error("hipMalloc(workspace): %s", hipGetErrorString(e));
+                rc = SMFV_ERR_HIP;
+            }
+            p->dev_bytes += p->ws_bytes;
+        }
+    } else if (h_row_ptr && h_col_idx && m > 0 && K > 0 && K % TILE_KP == 0 &&
+               !(flags & SMFV_PLAN_NO_TILES)) {
+        TileAnalysis T;
+        analyse_tiles(m, n, h_row_ptr, h_col_idx, T);
+        p->ntiles = (int)T.tile_direct.size();
+        p->union_rows = T.union_rows;
+        for (int t = 0; t < p->ntiles; ++t) {
+            if (T.tile_direct[t]) ++p->ndirect;
+            else p->tiled_nnz += h_row_ptr[T.tile_rows[t + 1]] - h_row_ptr[T.tile_rows[t]];
+        }
+        const double reuse = T.union_rows ? (double)p->tiled_nnz / (double)T.union_rows : 0.0;
+        // stage only when tiles re-use X rows enough to pay for the staging
+        if (reuse >= 1.25 || (flags & SMFV_PLAN_FORCE_TILES)) {
+            p->tiled = true;
+            if (!rc) rc = upload(&p->tile_rows, T.tile_rows, p->dev_bytes);
+            if (!rc) rc = upload(&p->tile_uoff, T.tile_uoff, p->dev_bytes);
+            if (!rc) rc = upload(&p->tile_direct, T.tile_direct, p->dev_bytes);
+            if (!rc) rc = upload(&p->ucols, T.ucols, p->dev_bytes);
+            if (!rc) rc = upload(&p->lidx, T.lidx, p->dev_bytes);
+        }
+    }
+    if (rc) {
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_plan_destroy(smfv_plan_t plan)
+{
+    delete plan;
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[6])
+{
+    SMFV_REQUIRE(plan && out, "null argument");
+    out[0] = plan->tiled ? 1.0 : 0.0;
+    out[1] = plan->ntiles;
+    out[2] = (double)plan->union_rows;
+    out[3] = plan->union_rows ? (double)plan->tiled_nnz / (double)plan->union_rows : 0.0;
+    out[4] = (double)plan->dev_bytes;
+    out[5] = plan->ndirect;
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int *d_col_idx,
+                               const double *d_values, const double *d_X, int64_t ldx,
+                               double *d_Y, int64_t ldy, void *stream)
+{
+    SMFV_REQUIRE(plan, "null plan");
+    const int m = plan->m, K = plan->K;
+    SMFV_REQUIRE(ldx >= K && ldy >= K, "leading dimension smaller than K");
+    if (m == 0 || K == 0) return SMFV_OK;
+    if (plan->tiled && pick_vec(d_X, ldx, d_Y, ldy, K) == 2) {
+        SMFV_REQUIRE(d_row_ptr && d_X && d_Y && d_values, "null argument");
+        hipLaunchKernelGGL(k_rows_tiled, dim3((unsigned)plan->ntiles, (unsigned)(K / TILE_KP)),
+                           dim3(256), 0, as_stream(stream), plan->tile_rows, plan->tile_uoff,
+                           plan->tile_direct, plan->ucols, plan->lidx, d_row_ptr, d_col_idx,
+                           d_values, d_X, ldx, K, d_Y, ldy);
+        SMFV_LAUNCHED();
+        return SMFV_OK;
+    }
+    return smfv_spmm_csr_f64(plan->variant, m, plan->n, plan->nnz, d_row_ptr, d_col_idx, d_values,
+                             d_X, ldx, K, d_Y, ldy, plan->ws, plan->ws_bytes, stream);
 }
 
 SMFV_API int smfv_spmm_rowblock_f64(int row_begin, int row_end, int n, const int *d_row_ptr,

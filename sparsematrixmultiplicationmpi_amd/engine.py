@@ -56,8 +56,9 @@ class DeviceCSR:
         A.validate()
         self.m, self.n, self.nnz = A.numRows, A.numCols, A.nnz
         self.h_row_ptr = np.ascontiguousarray(A.rowPtr, dtype=np.int32)
+        self.h_col_idx = np.ascontiguousarray(A.colIndices, dtype=np.int32)  # plan analysis
         self.row_ptr = torch.from_numpy(self.h_row_ptr).to(device)
-        self.col_idx = torch.from_numpy(np.ascontiguousarray(A.colIndices, dtype=np.int32)).to(device)
+        self.col_idx = torch.from_numpy(self.h_col_idx).to(device)
         self.values = torch.from_numpy(np.ascontiguousarray(A.values, dtype=np.float64)).to(device)
         self.device = device
 
@@ -85,26 +86,47 @@ def _check_dense(T: torch.Tensor, rows: int, K: int, name: str) -> int:
     return max(int(T.stride(0)), K)
 
 
-class SpmmPlan:
-    """Pre-sized execution of one variant for (A, K): the workspace is
-    allocated once so run() is a pure asynchronous launch sequence
-    (capturable into a hipGraph)."""
+PLAN_NO_TILES, PLAN_FORCE_TILES = 1, 2
 
-    def __init__(self, variant: int, A: DeviceCSR, K: int):
+
+class SpmmPlan:
+    """One variant of Y = A*X analysed once for (A, K) (smfv_plan_create):
+    device workspace allocated up front and, for K % 32 == 0, the row-tile
+    analysis that lets the kernel stage re-used X rows in LDS.  run() is a
+    pure asynchronous launch sequence (capturable into a hipGraph).
+
+    tiles: "auto" (stage when re-use >= 1.25), "off", or "force"."""
+
+    def __init__(self, variant: int, A: DeviceCSR, K: int, tiles: str = "auto"):
         self.variant, self.A, self.K = Variant(variant), A, K
-        nb = workspace_bytes(variant, A.m, A.nnz, K)
-        self.workspace = torch.empty(max(nb, 1), dtype=torch.uint8, device=A.device) if nb else None
-        self.ws_bytes = nb
+        flags = {"auto": 0, "off": PLAN_NO_TILES, "force": PLAN_FORCE_TILES}[tiles]
+        self._plan = ctypes.c_void_p()
+        ip = ctypes.POINTER(ctypes.c_int)
+        call("smfv_plan_create", byref(self._plan), int(variant), A.m, A.n, A.nnz,
+             A.h_row_ptr.ctypes.data_as(ip), A.h_col_idx.ctypes.data_as(ip), K, flags)
+
+    def stats(self) -> dict:
+        out = (ctypes.c_double * 6)()
+        call("smfv_plan_stats", self._plan, out)
+        return {"tiled": bool(out[0]), "tiles": int(out[1]), "staged_rows": int(out[2]),
+                "reuse": float(out[3]), "plan_bytes": int(out[4]), "direct_tiles": int(out[5])}
 
     def run(self, X: torch.Tensor, Y: torch.Tensor, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
         A, K = self.A, self.K
         ldx = _check_dense(X, A.n, K, "X")
         ldy = _check_dense(Y, A.m, K, "Y")
         rp, ci, va = A.ptrs()
-        ws = self.workspace.data_ptr() if self.workspace is not None else None
-        call("smfv_spmm_csr_f64", int(self.variant), A.m, A.n, A.nnz, rp, ci, va, X.data_ptr(), ldx,
-             K, Y.data_ptr(), ldy, ws, self.ws_bytes, stream_handle(stream))
+        call("smfv_plan_execute", self._plan, rp, ci, va, X.data_ptr(), ldx, Y.data_ptr(), ldy,
+             stream_handle(stream))
         return Y
+
+    def __del__(self):
+        try:
+            if self._plan:
+                call("smfv_plan_destroy", self._plan)
+                self._plan = ctypes.c_void_p()
+        except Exception:
+            pass
 
 
 def spmm(variant: int, A: DeviceCSR, X: torch.Tensor, Y: torch.Tensor | None = None,
