@@ -130,6 +130,8 @@ def main() -> None:
     ap.add_argument("--variant", default=None, choices=["SEQUENTIAL", "ROWWISE", "COLUMNWISE", "NONZERO"])
     ap.add_argument("--cold-bytes", type=float, default=1.0e9,
                     help="rotate copies until this many bytes separate two uses of one copy")
+    ap.add_argument("--tiles", default="auto", choices=["auto", "off", "force"],
+                    help="row-tile LDS staging of the plan (SpmmPlan tiles=)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -170,7 +172,7 @@ def main() -> None:
             dX = torch.empty((n, K), dtype=torch.float64, device=dev)
             smfv.fill_x_hash(dX, 43)
         dY = torch.empty((m, K), dtype=torch.float64, device=dev)
-        copies.append((smfv.SpmmPlan(smfv.Variant[variant], dA, K), dX, dY))
+        copies.append((smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles), dX, dY))
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
 

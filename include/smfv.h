@@ -103,7 +103,7 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz,
  * column indices.  The tiled kernel stages each tile's X rows once and reads
  * them from LDS -- same per-row order and arithmetic, bit-identical result.
  * Tiling is used when the measured re-use (non-zeros per staged X row) is
- * >= 1.25 or SMFV_PLAN_FORCE_TILES is set.  Creation allocates device memory
+ * >= 3 or SMFV_PLAN_FORCE_TILES is set.  Creation allocates device memory
  * and synchronises; execution is asynchronous and graph-capturable.  The
  * same d_row_ptr / d_col_idx / d_values the plan was built from must be
  * passed to every execute (the plan does not copy A). */

@@ -9,7 +9,10 @@ mkdir -p "$OUT/pmc_$TAG"
 export TMPDIR=/tmp
 cd /tmp
 i=0
-for ctrs in ${PMC_SETS:-"FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum" "SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_VALU SQ_WAVES"}; do
+# counter groups separated by ';'
+SETS=${PMC_SETS:-"FETCH_SIZE;WRITE_SIZE;TCC_HIT_sum TCC_MISS_sum;TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum;SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_VALU SQ_WAVES"}
+IFS=';' read -r -a GROUPS_ARR <<< "$SETS"
+for ctrs in "${GROUPS_ARR[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $ctrs -d "$OUT/pmc_$TAG/p$i" -o pmc --output-format csv \
      -- python3 "$ROOT/bench.py" --no-cpu-baseline --steps 20 --warmup 2 ${PMC_ARGS:-} > "$OUT/pmc_$TAG/p$i.log" 2>&1

@@ -47,7 +47,7 @@ def variants(A, K, dev, variant=smfv.Variant.ROWWISE, ncopies=8):
     copies = []
     for _ in range(ncopies):
         dA = smfv.DeviceCSR(A, dev)
-        copies.append((smfv.SpmmPlan(variant, dA, K), X.clone(), torch.empty((A.numRows, K), dtype=torch.float64, device=dev)))
+        copies.append((smfv.SpmmPlan(variant, dA, K, tiles=os.environ.get("LAB_TILES", "auto")), X.clone(), torch.empty((A.numRows, K), dtype=torch.float64, device=dev)))
     p, x, y = copies[0]
     warm = timeit(p, x, y)
     cold = timeit(p, x, y, copies=copies)

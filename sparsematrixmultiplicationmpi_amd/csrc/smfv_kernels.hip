@@ -324,18 +324,23 @@ __global__ __launch_bounds__(256) void k_rows_mh(int row_begin, int nrows,
 }
 
 // ---------------------------------------------------------------------------
-// k_rows_tiled: one workgroup per row tile (consecutive rows, see
+// k_rows_tiled: one workgroup per row tile (<= 32 consecutive rows, see
 // smfv_plan.cpp) and per 32-column panel of X / Y.
-//   1. the tile's distinct X rows (panel slice, 256 B each) are copied into
-//      LDS with LDS-DMA (global_load_lds_dwordx4: one wave-instruction moves
-//      4 rows = 1 KiB, lane-linear into a dense [u][32] image);
-//   2. a 16-lane team per row walks the row's non-zeros in CSR order: lane t
-//      holds (local column, value) of 16 consecutive non-zeros, broadcasts
-//      them inside the team (ds_bpermute) and reads the 16-byte X slice with
-//      one conflict-free ds_read_b128 (a 256-B row covers the 64 banks).
-// The X rows a tile re-uses are fetched from L2/HBM once instead of once per
-// non-zero; tiles whose union does not fit (one row wider than TILE_UCAP)
-// gather X directly.  Same per-row order and arithmetic as the reference.
+//   1. stage: the tile's distinct X rows (the panel's 256-B slice of each)
+//      are copied into a dense [u][32] LDS image with LDS-DMA
+//      (global_load_lds_dwordx4, 4 rows per wave-instruction), and the
+//      tile's non-zeros (16-bit local column, f64 value) into LDS;
+//   2. compute: an 8-lane team per row (8 rows per wave) walks the row's
+//      non-zeros in CSR order; lane t of team T holds columns
+//      {2t, 2t+1} of the two 128-B halves of the row, reading half
+//      (h ^ (T & 1)) in its h-th ds_read_b128, which makes every read of 8
+//      different X rows bank-conflict-free (the teams of one ds_read_b128
+//      lane group hit disjoint 16-bank quarters).
+// X rows re-used inside a tile come from L2/HBM once instead of once per
+// non-zero: the CU-side vector-memory path (~70 GB/s per CU for row
+// gathers, L1 hits included) is what bounds the untiled kernel.  Tiles that
+// exceed a cap (one very wide row) gather X directly.  Per-row order and
+// arithmetic are the reference's.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_rows_tiled(
     const int *__restrict__ tile_rows, const int *__restrict__ tile_uoff,
@@ -345,57 +350,94 @@ __global__ __launch_bounds__(256) void k_rows_tiled(
     double *__restrict__ Y, int64_t ldy)
 {
     __shared__ __attribute__((aligned(16))) double s_x[TILE_UCAP * TILE_KP];
+    __shared__ __attribute__((aligned(16))) double s_va[TILE_NCAP];
+    __shared__ uint16_t s_li[TILE_NCAP];
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int cp = blockIdx.y * TILE_KP;  // first column of this panel
     const int r0 = tile_rows[t], r1 = tile_rows[t + 1];
     const int u0 = tile_uoff[t], nu = tile_uoff[t + 1] - u0;
     const bool direct = tile_direct[t] != 0;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int tl = tid & 15, tbase = lane & ~15;
+    const int team = tid >> 3, tl = tid & 7, par = team & 1;
+    const int row = r0 + team;
+    const bool live = row < r1;
+    int js = 0, je = 0;
+    if (live) {
+        js = rp[row];
+        je = rp[row + 1];
+    }
+    double2 acc0 = make_double2(0.0, 0.0), acc1 = make_double2(0.0, 0.0);
     if (!direct) {
+        const int ts = rp[r0], tn = rp[r1] - ts;  // tile non-zeros (<= TILE_NCAP)
         for (int g = wave; g * 4 < nu; g += 4) {
             const int u = min(g * 4 + (lane >> 4), nu - 1);  // pad lanes re-read a valid row
-            const double *src = X + (int64_t)ucols[u0 + u] * ldx + cp + 2 * tl;
+            const double *src = X + (int64_t)ucols[u0 + u] * ldx + cp + 2 * (lane & 15);
             __builtin_amdgcn_global_load_lds(
                 (const void *)src, (__attribute__((address_space(3))) void *)(s_x + g * 128), 16, 0, 0);
         }
-    }
-    __syncthreads();  // drains the LDS-DMA (vmcnt(0)) and publishes the image
-    const int row = r0 + (tid >> 4);
-    if (row >= r1) return;
-    const int js = rp[row], je = rp[row + 1];
-    double2 acc = make_double2(0.0, 0.0);
-    if (!direct) {
-        constexpr int U = 8;
-        const double2 *sx = reinterpret_cast<const double2 *>(s_x) + tl;
-        for (int j0 = js; j0 < je; j0 += 16) {
-            const int n = min(16, je - j0);
-            int my_l = 0;
-            double my_v = 0.0;
-            if (tl < n) {
-                my_l = lidx[j0 + tl];
-                my_v = va[j0 + tl];
-            }
-            for (int t0 = 0; t0 < n; t0 += U) {
-                double2 x[U];
-                double v[U];
+        uint16_t rl[TILE_NCAP / 256];
+        double rv[TILE_NCAP / 256];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int src = tbase + min(t0 + u, 15);
-                    const int l = __shfl(my_l, src);
-                    v[u] = __shfl(my_v, src);
-                    x[u] = make_double2(0.0, 0.0);
-                    if (t0 + u < n) x[u] = sx[l * (TILE_KP / 2)];
-                }
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (t0 + u < n) acc = VecT<2>::madd(acc, v[u], x[u]);
+        for (int k = 0; k < TILE_NCAP / 256; ++k) {
+            const int e = k * 256 + tid;
+            rl[k] = 0;
+            rv[k] = 0.0;
+            if (e < tn) {
+                rl[k] = lidx[ts + e];
+                rv[k] = va[ts + e];
             }
         }
+#pragma unroll
+        for (int k = 0; k < TILE_NCAP / 256; ++k) {
+            const int e = k * 256 + tid;
+            if (e < tn) {
+                s_li[e] = rl[k];
+                s_va[e] = rv[k];
+            }
+        }
+        __syncthreads();  // drains the LDS-DMA (vmcnt(0)) and publishes the tile
+        if (!live) return;
+        constexpr int U = 8;
+        // this lane's 16-byte slot of half (h ^ par) of an X row, in double2 units
+        const double2 *sx0 = reinterpret_cast<const double2 *>(s_x) + par * 8 + tl;
+        const double2 *sx1 = reinterpret_cast<const double2 *>(s_x) + (par ^ 1) * 8 + tl;
+        const int a = js - ts, b = je - ts;
+        int j = a;
+        for (; j + U <= b; j += U) {
+            double2 x0[U], x1[U];
+            double v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int l = s_li[j + u];
+                v[u] = s_va[j + u];
+                x0[u] = sx0[l * (TILE_KP / 2)];
+                x1[u] = sx1[l * (TILE_KP / 2)];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                acc0 = VecT<2>::madd(acc0, v[u], x0[u]);
+                acc1 = VecT<2>::madd(acc1, v[u], x1[u]);
+            }
+        }
+        for (; j < b; ++j) {
+            const int l = s_li[j];
+            const double v = s_va[j];
+            acc0 = VecT<2>::madd(acc0, v, sx0[l * (TILE_KP / 2)]);
+            acc1 = VecT<2>::madd(acc1, v, sx1[l * (TILE_KP / 2)]);
+        }
     } else {
-        acc = row_segment<16, 2>(js, je, ci, va, X, ldx, cp + 2 * tl, true, acc);
+        if (!live) return;
+        // direct gathers: same lane -> column mapping as the LDS path
+        for (int j = js; j < je; ++j) {
+            const double *px = X + (int64_t)ci[j] * ldx + cp + 2 * tl;
+            const double v = va[j];
+            acc0 = VecT<2>::madd(acc0, v, *reinterpret_cast<const double2 *>(px + 16 * par));
+            acc1 = VecT<2>::madd(acc1, v, *reinterpret_cast<const double2 *>(px + 16 * (par ^ 1)));
+        }
     }
-    if (cp + 2 * tl < K) *reinterpret_cast<double2 *>(Y + (int64_t)row * ldy + cp + 2 * tl) = acc;
+    double *y = Y + (int64_t)row * ldy + cp + 2 * tl;
+    *reinterpret_cast<double2 *>(y + 16 * par) = acc0;
+    *reinterpret_cast<double2 *>(y + 16 * (par ^ 1)) = acc1;
 }
 
 // ---------------------------------------------------------------------------
@@ -853,6 +895,8 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz, const int
 // ---- plans (analysed once per matrix pattern and K) ------------------------
 }  // extern "C"
 
+constexpr double SMFV_TILE_MIN_REUSE = 3.0;
+
 struct smfv_plan_s {
     int variant = 0, m = 0, n = 0, K = 0;
     int64_t nnz = 0;
@@ -920,8 +964,10 @@ SMFV_API int smfv_plan_create(smfv_plan_t *out, int variant, int m, int n, int64
             else p->tiled_nnz += h_row_ptr[T.tile_rows[t + 1]] - h_row_ptr[T.tile_rows[t]];
         }
         const double reuse = T.union_rows ? (double)p->tiled_nnz / (double)T.union_rows : 0.0;
-        // stage only when tiles re-use X rows enough to pay for the staging
-        if (reuse >= 1.25 || (flags & SMFV_PLAN_FORCE_TILES)) {
+        // stage only when tiles re-use X rows enough to pay for the staging:
+        // measured on MI355X the untiled kernel sits at the CU row-gather
+        // ceiling and the tiled one wins only at high re-use
+        if (reuse >= SMFV_TILE_MIN_REUSE || (flags & SMFV_PLAN_FORCE_TILES)) {
             p->tiled = true;
             if (!rc) rc = upload(&p->tile_rows, T.tile_rows, p->dev_bytes);
             if (!rc) rc = upload(&p->tile_uoff, T.tile_uoff, p->dev_bytes);

@@ -30,6 +30,7 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
         const int r0 = i;
         const size_t ubase = A.ucols.size();
         int ucount = 0;
+        int64_t tnnz = 0;
         A.tile_rows.push_back(r0);
         A.tile_uoff.push_back((int)ubase);
         while (i < m && i - r0 < TILE_MAXROWS) {
@@ -43,7 +44,9 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
                     ++fresh;
                 }
             }
-            if (ucount + fresh > TILE_UCAP && i > r0) break;
+            const int64_t rlen = rp[i + 1] - rp[i];
+            if ((ucount + fresh > TILE_UCAP || tnnz + rlen > TILE_NCAP) && i > r0) break;
+            tnnz += rlen;
             for (int j = rp[i]; j < rp[i + 1]; ++j) {
                 const int c = ci[j];
                 if (stamp[c] != tile) {
@@ -54,9 +57,9 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
                 A.lidx[j] = (uint16_t)std::min(pos[c], 0xFFFF);
             }
             ++i;
-            if (ucount > TILE_UCAP) break;  // a single row wider than the LDS tile
+            if (ucount > TILE_UCAP || tnnz > TILE_NCAP) break;  // one row over a cap
         }
-        if (ucount > TILE_UCAP) {
+        if (ucount > TILE_UCAP || tnnz > TILE_NCAP) {
             A.ucols.resize(ubase);  // processed with direct X gathers
             A.tile_direct.push_back(1);
         } else {

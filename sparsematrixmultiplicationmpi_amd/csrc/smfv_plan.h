@@ -12,8 +12,10 @@ namespace smfv {
 constexpr int TILE_KP = 32;
 // Union capacity: distinct X rows of one tile held in LDS (128 x 256 B = 32 KiB).
 constexpr int TILE_UCAP = 128;
-// Rows per tile: one 16-lane team per row in a 256-lane block.
-constexpr int TILE_MAXROWS = 16;
+// Rows per tile: one 8-lane team per row in a 256-lane block.
+constexpr int TILE_MAXROWS = 32;
+// Non-zeros per tile staged in LDS (16-bit local column + f64 value).
+constexpr int TILE_NCAP = 1024;
 
 struct TileAnalysis {
     std::vector<int> tile_rows;    // T + 1 row boundaries (tiles are contiguous rows)
@@ -27,7 +29,8 @@ struct TileAnalysis {
 };
 
 // Greedy tiling of consecutive rows: grow a tile while its column union
-// stays <= TILE_UCAP and it has <= TILE_MAXROWS rows.
+// stays <= TILE_UCAP, its non-zeros <= TILE_NCAP and it has <= TILE_MAXROWS
+// rows.  A single row over either cap becomes a one-row "direct" tile.
 void analyse_tiles(int m, int n, const int *row_ptr, const int *col_idx, TileAnalysis &out);
 
 }  // namespace smfv
