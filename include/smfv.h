@@ -97,21 +97,30 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz,
 
 /* ---- plans: analysed once per (matrix pattern, K), executed many times --
  * The plan owns all device workspace (merge-path carries for NONZERO) and,
- * for SEQUENTIAL / ROWWISE / COLUMNWISE with K a multiple of 32, a row-tile
- * analysis of the pattern (h_col_idx needed): tiles of <= 16 consecutive
- * rows whose distinct X rows fit a 32 KiB LDS image, with 16-bit local
- * column indices.  The tiled kernel stages each tile's X rows once and reads
- * them from LDS -- same per-row order and arithmetic, bit-identical result.
- * Tiling is used when the measured re-use (non-zeros per staged X row) is
- * >= 3 or SMFV_PLAN_FORCE_TILES is set.  Creation allocates device memory
- * and synchronises; execution is asynchronous and graph-capturable.  The
- * same d_row_ptr / d_col_idx / d_values the plan was built from must be
- * passed to every execute (the plan does not copy A). */
+ * for SEQUENTIAL / ROWWISE / COLUMNWISE with K a multiple of 32, a clustered
+ * row-tile analysis of the pattern (h_col_idx needed): tiles of <= 32 rows
+ * grown by adjacency whose distinct X rows fit a 32 KiB LDS image, with a
+ * tile-ordered copy of the values and 16-bit union positions.  The tiled
+ * kernel stages each tile's X rows once and reads them from LDS -- same
+ * per-row order and arithmetic, bit-identical result.  Tiling is used when
+ * the re-use (non-zeros per staged X row) is >= 3 or SMFV_PLAN_FORCE_TILES
+ * is set.  A tiled plan must be bound to A's device values with
+ * smfv_plan_bind_values (and re-bound after they change); execute checks
+ * that it is given the bound pointer.  Creation allocates device memory and
+ * synchronises; bind and execute are asynchronous and graph-capturable. */
 typedef struct smfv_plan_s *smfv_plan_t;
 #define SMFV_PLAN_NO_TILES 1
 #define SMFV_PLAN_FORCE_TILES 2
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
+SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, void *stream);
+/* Host-only diagnostic: run the clustered tile analysis, verify the
+ * invariants the tiled kernel relies on (every row in exactly one tile, caps,
+ * CSR order inside rows, union positions) and report out[0] tiles, [1]
+ * staged X rows, [2] re-use, [3] direct tiles, [4] padded non-zeros,
+ * [5] non-zeros in staged tiles.  No device needed. */
+SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_col_idx,
+                               double out[6]);
 SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int *d_col_idx,
                                const double *d_values, const double *d_X, int64_t ldx,
                                double *d_Y, int64_t ldy, void *stream);

@@ -48,6 +48,8 @@ _SIGS = {
                                   c_void_p]),
     "smfv_plan_create": (c_int, [POINTER(c_void_p), c_int, c_int, c_int, c_int64, _PI, _PI, c_int,
                                  c_int]),
+    "smfv_plan_analyse": (c_int, [c_int, c_int, _PI, _PI, _PD]),
+    "smfv_plan_bind_values": (c_int, [c_void_p, c_void_p, c_void_p]),
     "smfv_plan_execute": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                   c_void_p, c_int64, c_void_p]),
     "smfv_plan_stats": (c_int, [c_void_p, _PD]),

@@ -324,86 +324,87 @@ __global__ __launch_bounds__(256) void k_rows_mh(int row_begin, int nrows,
 }
 
 // ---------------------------------------------------------------------------
-// k_rows_tiled: one workgroup per row tile (<= 32 consecutive rows, see
+// k_rows_tiled: one workgroup per row tile (<= 32 rows clustered by the plan,
 // smfv_plan.cpp) and per 32-column panel of X / Y.
-//   1. stage: the tile's distinct X rows (the panel's 256-B slice of each)
-//      are copied into a dense [u][32] LDS image with LDS-DMA
-//      (global_load_lds_dwordx4, 4 rows per wave-instruction), and the
-//      tile's non-zeros (16-bit local column, f64 value) into LDS;
-//   2. compute: an 8-lane team per row (8 rows per wave) walks the row's
-//      non-zeros in CSR order; lane t of team T holds columns
-//      {2t, 2t+1} of the two 128-B halves of the row, reading half
-//      (h ^ (T & 1)) in its h-th ds_read_b128, which makes every read of 8
-//      different X rows bank-conflict-free (the teams of one ds_read_b128
-//      lane group hit disjoint 16-bank quarters).
-// X rows re-used inside a tile come from L2/HBM once instead of once per
-// non-zero: the CU-side vector-memory path (~70 GB/s per CU for row
-// gathers, L1 hits included) is what bounds the untiled kernel.  Tiles that
-// exceed a cap (one very wide row) gather X directly.  Per-row order and
-// arithmetic are the reference's.
+//   0. the tile record (TileMeta, 32 B) is one scalar load;
+//   1. each lane loads the union ids of the X rows it will copy, plus (per
+//      team) its row id and tile-local non-zero range;
+//   2. LDS-DMA (global_load_lds_dwordx4): the tile's distinct X rows (the
+//      panel's 256-B slice each, 4 rows per wave-instruction) into a dense
+//      [u][32] image, and the tile's non-zeros -- tile-ordered copies of the
+//      values (f64) and 16-bit union positions owned by the plan -- into LDS;
+//   3. an 8-lane team per row (8 rows per wave) walks the row's non-zeros in
+//      CSR order; lane t of team T holds columns {2t, 2t+1} of both 128-B
+//      halves of the X row and reads half (h ^ (T & 1)) in its h-th
+//      ds_read_b128, which keeps the 8 rows a wave reads bank-conflict-free.
+// Each staged X row serves ~4 non-zeros on mesh-like patterns, so the
+// CU-side row-gather traffic (the bound of the untiled kernel) drops by that
+// factor.  A "direct" tile (one row over a cap) gathers X straight from HBM.
+// Per-row order and arithmetic are the reference's.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_rows_tiled(
-    const int *__restrict__ tile_rows, const int *__restrict__ tile_uoff,
-    const uint8_t *__restrict__ tile_direct, const int *__restrict__ ucols,
-    const uint16_t *__restrict__ lidx, const int *__restrict__ rp, const int *__restrict__ ci,
+    const TileMeta *__restrict__ meta, const int *__restrict__ trows, const int *__restrict__ rbeg,
+    const int *__restrict__ ucols, const uint16_t *__restrict__ tlidx,
+    const double *__restrict__ tvals, const int *__restrict__ rp, const int *__restrict__ ci,
     const double *__restrict__ va, const double *__restrict__ X, int64_t ldx, int K,
     double *__restrict__ Y, int64_t ldy)
 {
     __shared__ __attribute__((aligned(16))) double s_x[TILE_UCAP * TILE_KP];
     __shared__ __attribute__((aligned(16))) double s_va[TILE_NCAP];
-    __shared__ uint16_t s_li[TILE_NCAP];
+    __shared__ __attribute__((aligned(16))) uint16_t s_li[TILE_NCAP];
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int cp = blockIdx.y * TILE_KP;  // first column of this panel
-    const int r0 = tile_rows[t], r1 = tile_rows[t + 1];
-    const int u0 = tile_uoff[t], nu = tile_uoff[t + 1] - u0;
-    const bool direct = tile_direct[t] != 0;
+    const TileMeta tm = meta[t];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int team = tid >> 3, tl = tid & 7, par = team & 1;
-    const int row = r0 + team;
-    const bool live = row < r1;
-    int js = 0, je = 0;
+    const bool live = team < tm.nrows;
+    int row = 0, js = 0, je = 0;
     if (live) {
-        js = rp[row];
-        je = rp[row + 1];
+        row = trows[tm.roff + team];
+        js = rbeg[tm.roff + team];
+        je = team + 1 < tm.nrows ? rbeg[tm.roff + team + 1] : tm.tn;
     }
     double2 acc0 = make_double2(0.0, 0.0), acc1 = make_double2(0.0, 0.0);
-    if (!direct) {
-        const int ts = rp[r0], tn = rp[r1] - ts;  // tile non-zeros (<= TILE_NCAP)
-        for (int g = wave; g * 4 < nu; g += 4) {
-            const int u = min(g * 4 + (lane >> 4), nu - 1);  // pad lanes re-read a valid row
-            const double *src = X + (int64_t)ucols[u0 + u] * ldx + cp + 2 * (lane & 15);
-            __builtin_amdgcn_global_load_lds(
-                (const void *)src, (__attribute__((address_space(3))) void *)(s_x + g * 128), 16, 0, 0);
-        }
-        uint16_t rl[TILE_NCAP / 256];
-        double rv[TILE_NCAP / 256];
+    if (!tm.direct) {
+        // X rows: wave w copies groups g = w, w+4, ... of 4 union rows
+        constexpr int GPW = TILE_UCAP / 16;  // groups per wave
+        int src_row[GPW];
 #pragma unroll
-        for (int k = 0; k < TILE_NCAP / 256; ++k) {
-            const int e = k * 256 + tid;
-            rl[k] = 0;
-            rv[k] = 0.0;
-            if (e < tn) {
-                rl[k] = lidx[ts + e];
-                rv[k] = va[ts + e];
-            }
+        for (int k = 0; k < GPW; ++k) {
+            const int u = min((wave + 4 * k) * 4 + (lane >> 4), max(tm.nu - 1, 0));
+            src_row[k] = tm.nu > 0 ? ucols[tm.uoff + u] : 0;
         }
 #pragma unroll
-        for (int k = 0; k < TILE_NCAP / 256; ++k) {
-            const int e = k * 256 + tid;
-            if (e < tn) {
-                s_li[e] = rl[k];
-                s_va[e] = rv[k];
+        for (int k = 0; k < GPW; ++k) {
+            const int g = wave + 4 * k;
+            if (g * 4 < tm.nu) {
+                const double *src = X + (int64_t)src_row[k] * ldx + cp + 2 * (lane & 15);
+                __builtin_amdgcn_global_load_lds((const void *)src,
+                                                 (__attribute__((address_space(3))) void *)(s_x + g * 128),
+                                                 16, 0, 0);
             }
+        }
+        // values: 128 doubles per wave-instruction; local columns: 512 u16
+        const int tn8 = (tm.tn + 7) & ~7;  // padded segment (multiple of 8)
+        for (int v = wave; v * 128 < tn8; v += 4) {
+            const int e = min(v * 128 + 2 * lane, tn8 - 2);
+            __builtin_amdgcn_global_load_lds((const void *)(tvals + tm.noff + e),
+                                             (__attribute__((address_space(3))) void *)(s_va + v * 128),
+                                             16, 0, 0);
+        }
+        for (int v = wave; v * 512 < tn8; v += 4) {
+            const int e = min(v * 512 + 8 * lane, tn8 - 8);
+            __builtin_amdgcn_global_load_lds((const void *)(tlidx + tm.noff + e),
+                                             (__attribute__((address_space(3))) void *)(s_li + v * 512),
+                                             16, 0, 0);
         }
         __syncthreads();  // drains the LDS-DMA (vmcnt(0)) and publishes the tile
         if (!live) return;
         constexpr int U = 8;
-        // this lane's 16-byte slot of half (h ^ par) of an X row, in double2 units
         const double2 *sx0 = reinterpret_cast<const double2 *>(s_x) + par * 8 + tl;
         const double2 *sx1 = reinterpret_cast<const double2 *>(s_x) + (par ^ 1) * 8 + tl;
-        const int a = js - ts, b = je - ts;
-        int j = a;
-        for (; j + U <= b; j += U) {
+        int j = js;
+        for (; j + U <= je; j += U) {
             double2 x0[U], x1[U];
             double v[U];
 #pragma unroll
@@ -419,7 +420,7 @@ __global__ __launch_bounds__(256) void k_rows_tiled(
                 acc1 = VecT<2>::madd(acc1, v[u], x1[u]);
             }
         }
-        for (; j < b; ++j) {
+        for (; j < je; ++j) {
             const int l = s_li[j];
             const double v = s_va[j];
             acc0 = VecT<2>::madd(acc0, v, sx0[l * (TILE_KP / 2)]);
@@ -427,10 +428,10 @@ __global__ __launch_bounds__(256) void k_rows_tiled(
         }
     } else {
         if (!live) return;
-        // direct gathers: same lane -> column mapping as the LDS path
-        for (int j = js; j < je; ++j) {
-            const double *px = X + (int64_t)ci[j] * ldx + cp + 2 * tl;
-            const double v = va[j];
+        // one wide row: gather X directly, same lane -> column mapping
+        for (int jj = rp[row]; jj < rp[row + 1]; ++jj) {
+            const double *px = X + (int64_t)ci[jj] * ldx + cp + 2 * tl;
+            const double v = va[jj];
             acc0 = VecT<2>::madd(acc0, v, *reinterpret_cast<const double2 *>(px + 16 * par));
             acc1 = VecT<2>::madd(acc1, v, *reinterpret_cast<const double2 *>(px + 16 * (par ^ 1)));
         }
@@ -438,6 +439,18 @@ __global__ __launch_bounds__(256) void k_rows_tiled(
     double *y = Y + (int64_t)row * ldy + cp + 2 * tl;
     *reinterpret_cast<double2 *>(y + 16 * par) = acc0;
     *reinterpret_cast<double2 *>(y + 16 * (par ^ 1)) = acc1;
+}
+
+// plan value binding: tile-ordered copy of A's values (pads -> 0)
+__global__ __launch_bounds__(256) void k_gather_vals(int64_t count, const int *__restrict__ tsrc,
+                                                     const double *__restrict__ va,
+                                                     double *__restrict__ tvals)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < count) {
+        const int s = tsrc[i];
+        tvals[i] = s >= 0 ? va[s] : 0.0;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -896,22 +909,26 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz, const int
 }  // extern "C"
 
 constexpr double SMFV_TILE_MIN_REUSE = 3.0;
+constexpr int SMFV_TILE_SAMPLE_ROWS = 16384;  // rows analysed first to estimate re-use
 
 struct smfv_plan_s {
     int variant = 0, m = 0, n = 0, K = 0;
     int64_t nnz = 0;
     bool tiled = false;
     int ntiles = 0, ndirect = 0;
-    int64_t union_rows = 0, tiled_nnz = 0;
-    int *tile_rows = nullptr, *tile_uoff = nullptr, *ucols = nullptr;
-    uint8_t *tile_direct = nullptr;
-    uint16_t *lidx = nullptr;
+    int64_t union_rows = 0, tiled_nnz = 0, padded_nnz = 0;
+    double reuse = 0.0;
+    TileMeta *meta = nullptr;
+    int *trows = nullptr, *rbeg = nullptr, *ucols = nullptr, *tsrc = nullptr;
+    uint16_t *tlidx = nullptr;
+    double *tvals = nullptr;
+    const double *bound_values = nullptr;  // d_values the tile-ordered copy came from
     void *ws = nullptr;
     size_t ws_bytes = 0, dev_bytes = 0;
     ~smfv_plan_s()
     {
-        for (void *q : {(void *)tile_rows, (void *)tile_uoff, (void *)ucols, (void *)tile_direct,
-                        (void *)lidx, ws})
+        for (void *q : {(void *)meta, (void *)trows, (void *)rbeg, (void *)ucols, (void *)tsrc,
+                        (void *)tlidx, (void *)tvals, ws})
             if (q) (void)hipFree(q);
     }
 };
@@ -956,24 +973,42 @@ SMFV_API int smfv_plan_create(smfv_plan_t *out, int variant, int m, int n, int64
     } else if (h_row_ptr && h_col_idx && m > 0 && K > 0 && K % TILE_KP == 0 &&
                !(flags & SMFV_PLAN_NO_TILES)) {
         TileAnalysis T;
-        analyse_tiles(m, n, h_row_ptr, h_col_idx, T);
-        p->ntiles = (int)T.tile_direct.size();
-        p->union_rows = T.union_rows;
-        for (int t = 0; t < p->ntiles; ++t) {
-            if (T.tile_direct[t]) ++p->ndirect;
-            else p->tiled_nnz += h_row_ptr[T.tile_rows[t + 1]] - h_row_ptr[T.tile_rows[t]];
+        bool go = true;
+        if (!(flags & SMFV_PLAN_FORCE_TILES) && m > SMFV_TILE_SAMPLE_ROWS) {
+            // estimate re-use on a leading block of rows first (the analysis
+            // of the full pattern costs O(nnz * candidates))
+            const int ms = SMFV_TILE_SAMPLE_ROWS;
+            std::vector<int> rps(h_row_ptr, h_row_ptr + ms + 1);
+            analyse_tiles(ms, n, rps.data(), h_col_idx, T);
+            const double est = T.union_rows ? (double)T.tiled_nnz / (double)T.union_rows : 0.0;
+            go = est >= SMFV_TILE_MIN_REUSE;
         }
-        const double reuse = T.union_rows ? (double)p->tiled_nnz / (double)T.union_rows : 0.0;
-        // stage only when tiles re-use X rows enough to pay for the staging:
-        // measured on MI355X the untiled kernel sits at the CU row-gather
-        // ceiling and the tiled one wins only at high re-use
-        if (reuse >= SMFV_TILE_MIN_REUSE || (flags & SMFV_PLAN_FORCE_TILES)) {
-            p->tiled = true;
-            if (!rc) rc = upload(&p->tile_rows, T.tile_rows, p->dev_bytes);
-            if (!rc) rc = upload(&p->tile_uoff, T.tile_uoff, p->dev_bytes);
-            if (!rc) rc = upload(&p->tile_direct, T.tile_direct, p->dev_bytes);
-            if (!rc) rc = upload(&p->ucols, T.ucols, p->dev_bytes);
-            if (!rc) rc = upload(&p->lidx, T.lidx, p->dev_bytes);
+        if (go) {
+            analyse_tiles(m, n, h_row_ptr, h_col_idx, T);
+            p->ntiles = (int)T.meta.size();
+            p->union_rows = T.union_rows;
+            p->tiled_nnz = T.tiled_nnz;
+            p->padded_nnz = T.padded_nnz;
+            for (const TileMeta &tm : T.meta) p->ndirect += tm.direct;
+            p->reuse = T.union_rows ? (double)T.tiled_nnz / (double)T.union_rows : 0.0;
+            if (p->reuse >= SMFV_TILE_MIN_REUSE || (flags & SMFV_PLAN_FORCE_TILES)) {
+                p->tiled = true;
+                if (!rc) rc = upload(&p->meta, T.meta, p->dev_bytes);
+                if (!rc) rc = upload(&p->trows, T.trows, p->dev_bytes);
+                if (!rc) rc = upload(&p->rbeg, T.rbeg, p->dev_bytes);
+                if (!rc) rc = upload(&p->ucols, T.ucols, p->dev_bytes);
+                if (!rc) rc = upload(&p->tsrc, T.tsrc, p->dev_bytes);
+                if (!rc) rc = upload(&p->tlidx, T.tlidx, p->dev_bytes);
+                if (!rc) {
+                    const size_t b = std::max<size_t>((size_t)T.padded_nnz, 1) * sizeof(double);
+                    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p->tvals), b);
+                    if (e != hipSuccess) {
+                        set_error("hipMalloc(tvals): %s", hipGetErrorString(e));
+                        rc = SMFV_ERR_HIP;
+                    }
+                    p->dev_bytes += b;
+                }
+            }
         }
     }
     if (rc) {
@@ -981,6 +1016,65 @@ SMFV_API int smfv_plan_create(smfv_plan_t *out, int variant, int m, int n, int64
         return rc;
     }
     *out = p;
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_col_idx,
+                               double out[6])
+{
+    SMFV_REQUIRE(m >= 0 && n >= 0 && h_row_ptr && (h_row_ptr[m] == 0 || h_col_idx) && out,
+                 "bad argument");
+    TileAnalysis T;
+    analyse_tiles(m, n, h_row_ptr, h_col_idx, T);
+    // invariants the tiled kernel relies on
+    std::vector<char> seen((size_t)std::max(m, 1), 0);
+    int64_t nd = 0;
+    for (const TileMeta &tm : T.meta) {
+        SMFV_REQUIRE(tm.nrows >= 1 && tm.nrows <= TILE_MAXROWS, "tile rows out of range");
+        SMFV_REQUIRE(tm.noff % 8 == 0, "tile segment not 16-byte aligned");
+        if (tm.direct) {
+            ++nd;
+            SMFV_REQUIRE(tm.nrows == 1, "direct tile with several rows");
+        } else {
+            SMFV_REQUIRE(tm.nu <= TILE_UCAP && tm.tn <= TILE_NCAP, "tile over a cap");
+        }
+        int local = 0;
+        for (int k = 0; k < tm.nrows; ++k) {
+            const int r = T.trows[tm.roff + k];
+            SMFV_REQUIRE(r >= 0 && r < m && !seen[r], "row %d missing or in two tiles", r);
+            seen[r] = 1;
+            SMFV_REQUIRE(T.rbeg[tm.roff + k] == local, "row offsets inconsistent");
+            for (int j = h_row_ptr[r]; j < h_row_ptr[r + 1]; ++j, ++local) {
+                const int64_t e = (int64_t)tm.noff + local;
+                SMFV_REQUIRE(T.tsrc[e] == j, "tile order is not CSR order inside a row");
+                if (!tm.direct)
+                    SMFV_REQUIRE(T.ucols[tm.uoff + T.tlidx[e]] == h_col_idx[j], "bad union position");
+            }
+        }
+        SMFV_REQUIRE(local == tm.tn, "tile non-zero count");
+    }
+    for (int r = 0; r < m; ++r) SMFV_REQUIRE(seen[r], "row %d in no tile", r);
+    out[0] = (double)T.meta.size();
+    out[1] = (double)T.union_rows;
+    out[2] = T.union_rows ? (double)T.tiled_nnz / (double)T.union_rows : 0.0;
+    out[3] = (double)nd;
+    out[4] = (double)T.padded_nnz;
+    out[5] = (double)T.tiled_nnz;
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, void *stream)
+{
+    SMFV_REQUIRE(plan, "null plan");
+    if (!plan->tiled) return SMFV_OK;
+    SMFV_REQUIRE(d_values || plan->nnz == 0, "null values");
+    const int64_t cnt = plan->padded_nnz;
+    if (cnt > 0) {
+        hipLaunchKernelGGL(k_gather_vals, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0,
+                           as_stream(stream), cnt, plan->tsrc, d_values, plan->tvals);
+        SMFV_LAUNCHED();
+    }
+    plan->bound_values = d_values;
     return SMFV_OK;
 }
 
@@ -996,7 +1090,7 @@ SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[6])
     out[0] = plan->tiled ? 1.0 : 0.0;
     out[1] = plan->ntiles;
     out[2] = (double)plan->union_rows;
-    out[3] = plan->union_rows ? (double)plan->tiled_nnz / (double)plan->union_rows : 0.0;
+    out[3] = plan->reuse;
     out[4] = (double)plan->dev_bytes;
     out[5] = plan->ndirect;
     return SMFV_OK;
@@ -1012,10 +1106,14 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     if (m == 0 || K == 0) return SMFV_OK;
     if (plan->tiled && pick_vec(d_X, ldx, d_Y, ldy, K) == 2) {
         SMFV_REQUIRE(d_row_ptr && d_X && d_Y && d_values, "null argument");
+        if (d_values != plan->bound_values) {
+            set_error("tiled plan: values not bound (call smfv_plan_bind_values with these d_values)");
+            return SMFV_ERR_INVALID;
+        }
         hipLaunchKernelGGL(k_rows_tiled, dim3((unsigned)plan->ntiles, (unsigned)(K / TILE_KP)),
-                           dim3(256), 0, as_stream(stream), plan->tile_rows, plan->tile_uoff,
-                           plan->tile_direct, plan->ucols, plan->lidx, d_row_ptr, d_col_idx,
-                           d_values, d_X, ldx, K, d_Y, ldy);
+                           dim3(256), 0, as_stream(stream), plan->meta, plan->trows, plan->rbeg,
+                           plan->ucols, plan->tlidx, plan->tvals, d_row_ptr, d_col_idx, d_values,
+                           d_X, ldx, K, d_Y, ldy);
         SMFV_LAUNCHED();
         return SMFV_OK;
     }

@@ -1,12 +1,16 @@
-// smfv_plan.cpp -- row-tile analysis of a CSR pattern (host, O(nnz)).
+// smfv_plan.cpp -- clustered row-tile analysis of a CSR pattern (host).
 //
-// The LDS-tiled row kernel processes a tile of consecutive rows in one
-// workgroup: the distinct X rows the tile touches are staged into LDS once
-// and every non-zero of the tile reads its X row from LDS.  This pass
-// decides the tiles (greedy: grow while the column union fits TILE_UCAP and
-// the tile has at most TILE_MAXROWS rows) and re-expresses every column
-// index as a 16-bit position in its tile's union list.  Computation order is
-// untouched: each row is still summed over its non-zeros in CSR order.
+// The LDS-tiled row kernel processes a tile of rows in one workgroup: the
+// distinct X rows the tile touches are staged into LDS once and every
+// non-zero of the tile reads its X row from LDS.  Its speed is set by how
+// many non-zeros share each staged row (re-use), so tiles are grown as
+// clusters: starting from the first unassigned row, repeatedly add the
+// candidate row that brings the fewest new columns into the tile's union.
+// Candidates are the rows named by the tile's columns (for a square pattern,
+// graph neighbours), which for mesh-like matrices grows compact 3-D blocks
+// (re-use ~4.3 at a 128-row union on the cop20k_A surrogate, against ~2.1
+// for runs of consecutive rows).  Each row is still summed over its
+// non-zeros in CSR order, so results are bit-identical.
 #include "smfv_plan.h"
 
 #include <algorithm>
@@ -15,61 +19,104 @@ namespace smfv {
 
 void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
 {
-    A.tile_rows.clear();
-    A.tile_uoff.clear();
-    A.tile_direct.clear();
-    A.ucols.clear();
-    A.lidx.assign((size_t)(m > 0 ? rp[m] : 0), 0);
-    A.union_rows = 0;
-    // stamp[c] == tile id  <=> column c already in the current tile's union;
-    // a negative stamp marks "seen while testing a row" (never a tile id)
-    std::vector<int> stamp((size_t)std::max(n, 1), -1), pos((size_t)std::max(n, 1), 0);
+    A = TileAnalysis();
+    const int ncol = std::max(n, 1);
+    std::vector<char> assigned((size_t)std::max(m, 1), 0);
+    std::vector<int> ustamp((size_t)ncol, -1);      // column in current tile union
+    std::vector<int> upos((size_t)ncol, 0);         // its position in the union
+    std::vector<int> cstamp((size_t)std::max(m, 1), -1);  // row already a candidate
+    std::vector<int64_t> probe((size_t)ncol, -1);   // column counted in a probe
+    std::vector<int> cand, rows;
+    int64_t probe_id = 0;
     int tile = 0;
-    int i = 0;
-    while (i < m) {
-        const int r0 = i;
-        const size_t ubase = A.ucols.size();
+
+    for (int seed = 0; seed < m; ++seed) {
+        if (assigned[seed]) continue;
         int ucount = 0;
         int64_t tnnz = 0;
-        A.tile_rows.push_back(r0);
-        A.tile_uoff.push_back((int)ubase);
-        while (i < m && i - r0 < TILE_MAXROWS) {
-            // distinct columns of row i not yet in the tile
-            const int probe = -2 - tile;
-            int fresh = 0;
-            for (int j = rp[i]; j < rp[i + 1]; ++j) {
+        rows.clear();
+        cand.clear();
+        const size_t ubase = A.ucols.size();
+        auto add_row = [&](int r) {
+            assigned[r] = 1;
+            rows.push_back(r);
+            tnnz += rp[r + 1] - rp[r];
+            for (int j = rp[r]; j < rp[r + 1]; ++j) {
                 const int c = ci[j];
-                if (stamp[c] != tile && stamp[c] != probe) {
-                    stamp[c] = probe;
-                    ++fresh;
-                }
-            }
-            const int64_t rlen = rp[i + 1] - rp[i];
-            if ((ucount + fresh > TILE_UCAP || tnnz + rlen > TILE_NCAP) && i > r0) break;
-            tnnz += rlen;
-            for (int j = rp[i]; j < rp[i + 1]; ++j) {
-                const int c = ci[j];
-                if (stamp[c] != tile) {
-                    stamp[c] = tile;
-                    pos[c] = ucount++;
+                if (ustamp[c] != tile) {
+                    ustamp[c] = tile;
+                    upos[c] = ucount++;
                     A.ucols.push_back(c);
                 }
-                A.lidx[j] = (uint16_t)std::min(pos[c], 0xFFFF);
+                if (c < m && !assigned[c] && cstamp[c] != tile) {
+                    cstamp[c] = tile;
+                    cand.push_back(c);
+                }
             }
-            ++i;
-            if (ucount > TILE_UCAP || tnnz > TILE_NCAP) break;  // one row over a cap
+        };
+        add_row(seed);
+        const bool over = ucount > TILE_UCAP || tnnz > TILE_NCAP;
+        while (!over && (int)rows.size() < TILE_MAXROWS) {
+            int best = -1, best_fresh = 1 << 30;
+            for (int r : cand) {
+                if (assigned[r]) continue;
+                ++probe_id;
+                int fresh = 0;
+                for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                    const int c = ci[j];
+                    if (ustamp[c] != tile && probe[c] != probe_id) {
+                        probe[c] = probe_id;
+                        ++fresh;
+                    }
+                }
+                if (fresh < best_fresh || (fresh == best_fresh && r < best)) {
+                    best_fresh = fresh;
+                    best = r;
+                }
+            }
+            if (best < 0) break;
+            if (ucount + best_fresh > TILE_UCAP || tnnz + (rp[best + 1] - rp[best]) > TILE_NCAP) break;
+            add_row(best);
         }
-        if (ucount > TILE_UCAP || tnnz > TILE_NCAP) {
-            A.ucols.resize(ubase);  // processed with direct X gathers
-            A.tile_direct.push_back(1);
+        std::sort(rows.begin(), rows.end());
+
+        TileMeta tm{};
+        tm.roff = (int)A.trows.size();
+        tm.nrows = (int)rows.size();
+        tm.noff = (int)A.padded_nnz;
+        tm.tn = (int)tnnz;
+        tm.direct = over ? 1 : 0;
+        if (over) {
+            A.ucols.resize(ubase);
+            tm.uoff = (int)ubase;
+            tm.nu = 0;
         } else {
-            A.tile_direct.push_back(0);
+            tm.uoff = (int)ubase;
+            tm.nu = ucount;
             A.union_rows += ucount;
+            A.tiled_nnz += tnnz;
         }
+        int local = 0;
+        for (int r : rows) {
+            A.trows.push_back(r);
+            A.rbeg.push_back(local);
+            for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                A.tsrc.push_back(j);
+                A.tlidx.push_back(over ? 0 : (uint16_t)upos[ci[j]]);
+                ++local;
+            }
+        }
+        // pad each tile's segment to a multiple of 8 entries (16-byte aligned
+        // starts for the u16 and f64 LDS-DMA copies)
+        while (local % 8) {
+            A.tsrc.push_back(-1);
+            A.tlidx.push_back(0);
+            ++local;
+        }
+        A.padded_nnz += local;
+        A.meta.push_back(tm);
         ++tile;
     }
-    A.tile_rows.push_back(m);
-    A.tile_uoff.push_back((int)A.ucols.size());
 }
 
 }  // namespace smfv

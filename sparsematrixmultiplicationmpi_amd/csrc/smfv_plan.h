@@ -1,5 +1,5 @@
-// smfv_plan.h -- internal: row-tile analysis of a CSR pattern for the
-// LDS-tiled row kernel (X-row reuse inside a tile of consecutive rows).
+// smfv_plan.h -- internal: clustered row-tile analysis of a CSR pattern for
+// the LDS-tiled row kernel (X-row re-use inside a tile of rows).
 #pragma once
 
 #include <cstdint>
@@ -7,8 +7,7 @@
 
 namespace smfv {
 
-// Column-panel width the tiled kernel stages per X row (32 doubles = 256 B,
-// a 16-lane team reads one row with one ds_read_b128 per lane).
+// Column-panel width the tiled kernel stages per X row (32 doubles = 256 B).
 constexpr int TILE_KP = 32;
 // Union capacity: distinct X rows of one tile held in LDS (128 x 256 B = 32 KiB).
 constexpr int TILE_UCAP = 128;
@@ -17,20 +16,37 @@ constexpr int TILE_MAXROWS = 32;
 // Non-zeros per tile staged in LDS (16-bit local column + f64 value).
 constexpr int TILE_NCAP = 1024;
 
-struct TileAnalysis {
-    std::vector<int> tile_rows;    // T + 1 row boundaries (tiles are contiguous rows)
-    std::vector<int> tile_uoff;    // T + 1 offsets into ucols; a tile whose union
-                                   // exceeds TILE_UCAP gets an empty range and is
-                                   // processed with direct gathers (tile_direct)
-    std::vector<uint8_t> tile_direct;
-    std::vector<int> ucols;        // distinct columns of each tile, first-use order
-    std::vector<uint16_t> lidx;    // per non-zero: position of its column in its tile's ucols
-    int64_t union_rows = 0;        // sum of tile unions (X rows staged per panel)
+// Per-tile record (32 bytes), read with one scalar load by the kernel.
+struct TileMeta {
+    int32_t noff;   // start of the tile's non-zeros in tvals / tlidx (multiple of 8)
+    int32_t tn;     // non-zeros in the tile
+    int32_t uoff;   // start of the tile's union in ucols
+    int32_t nu;     // distinct X rows (0 for a direct tile)
+    int32_t roff;   // start of the tile's rows in trows / rbeg
+    int32_t nrows;  // rows in the tile
+    int32_t direct; // 1: one row over a cap, gathered straight from X
+    int32_t pad;
 };
 
-// Greedy tiling of consecutive rows: grow a tile while its column union
-// stays <= TILE_UCAP, its non-zeros <= TILE_NCAP and it has <= TILE_MAXROWS
-// rows.  A single row over either cap becomes a one-row "direct" tile.
+struct TileAnalysis {
+    std::vector<TileMeta> meta;
+    std::vector<int> trows;        // rows of each tile (any order of the matrix rows)
+    std::vector<int> rbeg;         // per tile row: first non-zero, tile-local
+    std::vector<int> ucols;        // distinct columns of each tile, first-use order
+    std::vector<int> tsrc;         // per tile-ordered non-zero: its index in the CSR arrays
+    std::vector<uint16_t> tlidx;   // per tile-ordered non-zero: position in its tile's ucols
+    int64_t union_rows = 0;        // sum of tile unions (X rows staged per panel)
+    int64_t tiled_nnz = 0;         // non-zeros in non-direct tiles
+    int64_t padded_nnz = 0;        // length of tvals / tlidx / tsrc
+};
+
+// Clustered tiling: seed a tile at the first unassigned row, then repeatedly
+// add the candidate row (a column index of a row already in the tile, i.e. a
+// graph neighbour for square patterns) that adds the fewest new columns to
+// the tile's union, while union <= TILE_UCAP, non-zeros <= TILE_NCAP and
+// rows <= TILE_MAXROWS.  A row over a cap alone becomes a one-row "direct"
+// tile.  Every row lands in exactly one tile; the per-row non-zero order is
+// the CSR order, so results are unchanged.
 void analyse_tiles(int m, int n, const int *row_ptr, const int *col_idx, TileAnalysis &out);
 
 }  // namespace smfv

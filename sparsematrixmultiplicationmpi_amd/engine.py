@@ -95,7 +95,7 @@ class SpmmPlan:
     analysis that lets the kernel stage re-used X rows in LDS.  run() is a
     pure asynchronous launch sequence (capturable into a hipGraph).
 
-    tiles: "auto" (stage when re-use >= 1.25), "off", or "force"."""
+    tiles: "auto" (stage when re-use >= 3), "off", or "force"."""
 
     def __init__(self, variant: int, A: DeviceCSR, K: int, tiles: str = "auto"):
         self.variant, self.A, self.K = Variant(variant), A, K
@@ -104,6 +104,11 @@ class SpmmPlan:
         ip = ctypes.POINTER(ctypes.c_int)
         call("smfv_plan_create", byref(self._plan), int(variant), A.m, A.n, A.nnz,
              A.h_row_ptr.ctypes.data_as(ip), A.h_col_idx.ctypes.data_as(ip), K, flags)
+        self.bind_values()
+
+    def bind_values(self, stream: torch.cuda.Stream | None = None) -> None:
+        """(Re)bind a tiled plan to A's current device values (after they change)."""
+        call("smfv_plan_bind_values", self._plan, self.A.values.data_ptr(), stream_handle(stream))
 
     def stats(self) -> dict:
         out = (ctypes.c_double * 6)()

@@ -189,3 +189,28 @@ def test_product_has_no_oracle_dependency():
                 assert "oracle" not in src.lower().replace("oracle_", ""), f
     nm = subprocess.run(["nm", "-D", os.path.join(PKG, "libsmfv.so")], capture_output=True, text=True).stdout
     assert "oracle_" not in nm
+
+
+def _analyse(A):
+    out = (ctypes.c_double * 6)()
+    ip = ctypes.POINTER(ctypes.c_int)
+    _lib.call("smfv_plan_analyse", A.numRows, A.numCols, A.rowPtr.ctypes.data_as(ip),
+              A.colIndices.ctypes.data_as(ip), out)
+    return list(out)
+
+
+def test_tile_analysis_invariants_and_reuse():
+    """Clustered row tiles: the native analysis verifies its own invariants
+    (every row in one tile, caps, CSR order, union positions) and reports
+    re-use; adjacency clustering must beat runs of consecutive rows."""
+    tiles, staged, reuse, direct, padded, tiled_nnz = _analyse(smfv.cop20k_surrogate())
+    assert reuse > 4.0 and direct == 0 and padded % 8 == 0
+    # wide rows become direct tiles, random patterns have no re-use
+    B = smfv.gen_random_rows(20000, 20000, 16, 2.0, 4096, 42)
+    tiles, staged, reuse, direct, padded, tiled_nnz = _analyse(B)
+    assert direct > 0 and reuse < 1.5
+    # empty rows, rectangular, duplicates
+    A = smfv.readMatrixMarketFile(os.path.join(GOLDEN, "pat4x6.mtx"))
+    assert _analyse(A)[0] >= 1
+    A = smfv.readMatrixMarketFile(os.path.join(GOLDEN, "empty7x5.mtx"))
+    assert _analyse(A)[0] >= 1
