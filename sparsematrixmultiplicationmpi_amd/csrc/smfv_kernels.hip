@@ -342,6 +342,7 @@ __global__ __launch_bounds__(256) void k_rows_mh(int row_begin, int nrows,
 // factor.  A "direct" tile (one row over a cap) gathers X straight from HBM.
 // Per-row order and arithmetic are the reference's.
 // ---------------------------------------------------------------------------
+template <int MODE>  // 0 = production; lab ablations: 1 = stage only, 2 = compute only
 __global__ __launch_bounds__(256) void k_rows_tiled(
     const TileMeta *__restrict__ meta, const int *__restrict__ trows, const int *__restrict__ rbeg,
     const int *__restrict__ ucols, const uint16_t *__restrict__ tlidx,
@@ -368,6 +369,7 @@ __global__ __launch_bounds__(256) void k_rows_tiled(
     if (!tm.direct) {
         // X rows: wave w copies groups g = w, w+4, ... of 4 union rows
         constexpr int GPW = TILE_UCAP / 16;  // groups per wave
+        if constexpr (MODE != 2) {
         int src_row[GPW];
 #pragma unroll
         for (int k = 0; k < GPW; ++k) {
@@ -398,9 +400,11 @@ __global__ __launch_bounds__(256) void k_rows_tiled(
                                              (__attribute__((address_space(3))) void *)(s_li + v * 512),
                                              16, 0, 0);
         }
+        }  // MODE != 2
         __syncthreads();  // drains the LDS-DMA (vmcnt(0)) and publishes the tile
         if (!live) return;
         constexpr int U = 8;
+        if constexpr (MODE == 1) je = js;  // lab: stage only
         const double2 *sx0 = reinterpret_cast<const double2 *>(s_x) + par * 8 + tl;
         const double2 *sx1 = reinterpret_cast<const double2 *>(s_x) + (par ^ 1) * 8 + tl;
         int j = js;
@@ -1110,7 +1114,12 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             set_error("tiled plan: values not bound (call smfv_plan_bind_values with these d_values)");
             return SMFV_ERR_INVALID;
         }
-        hipLaunchKernelGGL(k_rows_tiled, dim3((unsigned)plan->ntiles, (unsigned)(K / TILE_KP)),
+        static const int ablate = [] {  // lab-only A/B of the two phases
+            const char *e = std::getenv("SMFV_TILED_ABLATE");
+            return e ? std::atoi(e) : 0;
+        }();
+        auto kern = ablate == 1 ? k_rows_tiled<1> : ablate == 2 ? k_rows_tiled<2> : k_rows_tiled<0>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)plan->ntiles, (unsigned)(K / TILE_KP)),
                            dim3(256), 0, as_stream(stream), plan->meta, plan->trows, plan->rbeg,
                            plan->ucols, plan->tlidx, plan->tvals, d_row_ptr, d_col_idx, d_values,
                            d_X, ldx, K, d_Y, ldy);

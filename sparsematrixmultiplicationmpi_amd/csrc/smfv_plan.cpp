@@ -30,8 +30,10 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
     int64_t probe_id = 0;
     int tile = 0;
 
+    int next_free = 0;
     for (int seed = 0; seed < m; ++seed) {
         if (assigned[seed]) continue;
+        next_free = seed + 1;
         int ucount = 0;
         int64_t tnnz = 0;
         rows.clear();
@@ -74,7 +76,22 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
                     best = r;
                 }
             }
-            if (best < 0) break;
+            if (best < 0) {
+                // no neighbour left (e.g. a diagonal or block-diagonal pattern):
+                // continue with the next unassigned row in natural order
+                while (next_free < m && assigned[next_free]) ++next_free;
+                if (next_free >= m) break;
+                best = next_free;
+                ++probe_id;
+                best_fresh = 0;
+                for (int j = rp[best]; j < rp[best + 1]; ++j) {
+                    const int c = ci[j];
+                    if (ustamp[c] != tile && probe[c] != probe_id) {
+                        probe[c] = probe_id;
+                        ++best_fresh;
+                    }
+                }
+            }
             if (ucount + best_fresh > TILE_UCAP || tnnz + (rp[best + 1] - rp[best]) > TILE_NCAP) break;
             add_row(best);
         }
