@@ -362,8 +362,9 @@ __global__ __launch_bounds__(256) void k_rows_tiled(
     int row = 0, js = 0, je = 0;
     if (live) {
         row = trows[tm.roff + team];
-        js = rbeg[tm.roff + team];
-        je = team + 1 < tm.nrows ? rbeg[tm.roff + team + 1] : tm.tn;
+        const int info = rbeg[tm.roff + team];  // start (multiple of 8) | len << 16
+        js = info & 0xFFFF;
+        je = js + (info >> 16);
     }
     double2 acc0 = make_double2(0.0, 0.0), acc1 = make_double2(0.0, 0.0);
     if (!tm.direct) {
@@ -1047,13 +1048,17 @@ SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_
             const int r = T.trows[tm.roff + k];
             SMFV_REQUIRE(r >= 0 && r < m && !seen[r], "row %d missing or in two tiles", r);
             seen[r] = 1;
-            SMFV_REQUIRE(T.rbeg[tm.roff + k] == local, "row offsets inconsistent");
+            const int info = T.rbeg[tm.roff + k];
+            SMFV_REQUIRE((info & 0xFFFF) == (local & 0xFFFF) && local % 8 == 0 &&
+                             (tm.direct || (info >> 16) == h_row_ptr[r + 1] - h_row_ptr[r]),
+                         "row offsets inconsistent");
             for (int j = h_row_ptr[r]; j < h_row_ptr[r + 1]; ++j, ++local) {
                 const int64_t e = (int64_t)tm.noff + local;
                 SMFV_REQUIRE(T.tsrc[e] == j, "tile order is not CSR order inside a row");
                 if (!tm.direct)
                     SMFV_REQUIRE(T.ucols[tm.uoff + T.tlidx[e]] == h_col_idx[j], "bad union position");
             }
+            for (; local % 8; ++local) SMFV_REQUIRE(T.tsrc[(int64_t)tm.noff + local] == -1, "bad pad");
         }
         SMFV_REQUIRE(local == tm.tn, "tile non-zero count");
     }

@@ -35,7 +35,7 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
         if (assigned[seed]) continue;
         next_free = seed + 1;
         int ucount = 0;
-        int64_t tnnz = 0;
+        int64_t tnnz = 0, tpad = 0;  // real and row-padded non-zeros
         rows.clear();
         cand.clear();
         const size_t ubase = A.ucols.size();
@@ -43,6 +43,7 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
             assigned[r] = 1;
             rows.push_back(r);
             tnnz += rp[r + 1] - rp[r];
+            tpad += (rp[r + 1] - rp[r] + 7) & ~7;
             for (int j = rp[r]; j < rp[r + 1]; ++j) {
                 const int c = ci[j];
                 if (ustamp[c] != tile) {
@@ -57,7 +58,7 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
             }
         };
         add_row(seed);
-        const bool over = ucount > TILE_UCAP || tnnz > TILE_NCAP;
+        const bool over = ucount > TILE_UCAP || tpad > TILE_NCAP;
         while (!over && (int)rows.size() < TILE_MAXROWS) {
             int best = -1, best_fresh = 1 << 30;
             for (int r : cand) {
@@ -92,7 +93,9 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
                     }
                 }
             }
-            if (ucount + best_fresh > TILE_UCAP || tnnz + (rp[best + 1] - rp[best]) > TILE_NCAP) break;
+            if (ucount + best_fresh > TILE_UCAP ||
+                tpad + ((rp[best + 1] - rp[best] + 7) & ~7) > TILE_NCAP)
+                break;
             add_row(best);
         }
         std::sort(rows.begin(), rows.end());
@@ -113,23 +116,29 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
             A.union_rows += ucount;
             A.tiled_nnz += tnnz;
         }
+        // tile-ordered non-zeros; every ROW segment starts at a multiple of 8
+        // entries, so the kernel's 8-wide batches of u16 / f64 LDS reads are
+        // 16-byte aligned (unaligned wide LDS reads are replayed); pads
+        // (tsrc = -1) are never summed: loops stop at the row's real length
         int local = 0;
         for (int r : rows) {
             A.trows.push_back(r);
-            A.rbeg.push_back(local);
+            // packed (tile-local start, length); a direct tile's lengths are
+            // not used (the kernel reads row_ptr there)
+            const int len = rp[r + 1] - rp[r];
+            A.rbeg.push_back(over ? local : (local | (len << 16)));
             for (int j = rp[r]; j < rp[r + 1]; ++j) {
                 A.tsrc.push_back(j);
                 A.tlidx.push_back(over ? 0 : (uint16_t)upos[ci[j]]);
                 ++local;
             }
+            while (local % 8) {
+                A.tsrc.push_back(-1);
+                A.tlidx.push_back(0);
+                ++local;
+            }
         }
-        // pad each tile's segment to a multiple of 8 entries (16-byte aligned
-        // starts for the u16 and f64 LDS-DMA copies)
-        while (local % 8) {
-            A.tsrc.push_back(-1);
-            A.tlidx.push_back(0);
-            ++local;
-        }
+        tm.tn = local;  // padded segment length (row ends come from rbeg / rp)
         A.padded_nnz += local;
         A.meta.push_back(tm);
         ++tile;

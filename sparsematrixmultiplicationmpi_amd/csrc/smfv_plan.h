@@ -19,7 +19,7 @@ constexpr int TILE_NCAP = 1024;
 // Per-tile record (32 bytes), read with one scalar load by the kernel.
 struct TileMeta {
     int32_t noff;   // start of the tile's non-zeros in tvals / tlidx (multiple of 8)
-    int32_t tn;     // non-zeros in the tile
+    int32_t tn;     // length of the tile's segment (rows padded to multiples of 8)
     int32_t uoff;   // start of the tile's union in ucols
     int32_t nu;     // distinct X rows (0 for a direct tile)
     int32_t roff;   // start of the tile's rows in trows / rbeg
@@ -31,7 +31,7 @@ struct TileMeta {
 struct TileAnalysis {
     std::vector<TileMeta> meta;
     std::vector<int> trows;        // rows of each tile (any order of the matrix rows)
-    std::vector<int> rbeg;         // per tile row: first non-zero, tile-local
+    std::vector<int> rbeg;         // per tile row: tile-local start | (length << 16)
     std::vector<int> ucols;        // distinct columns of each tile, first-use order
     std::vector<int> tsrc;         // per tile-ordered non-zero: its index in the CSR arrays
     std::vector<uint16_t> tlidx;   // per tile-ordered non-zero: position in its tile's ucols
