@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Lab: phase ablation of the tiled kernel (SMFV_TILED_ABLATE = 0 full,
-1 stage only, 2 compute only), one process per mode; plus the untiled
-kernel for reference.  Not part of the product or the bench."""
+"""Lab: the tiled kernels (SMFV_TILED_ABLATE = 0 pipelined persistent,
+1 one-shot, 2 one-shot stage only, 3 one-shot compute only), one process per
+mode; plus the untiled kernel for reference.  Not part of the product or the bench."""
 import json
 import os
 import subprocess
@@ -19,8 +19,13 @@ A = smfv.cop20k_surrogate()
 w, c = variants(A, 32, dev)
 print("RESULT " + json.dumps({"mode": MODE, "warm_us": round(w, 2), "cold_us": round(c, 2)}))
 '''
-for mode, env in (("full", {"SMFV_TILED_ABLATE": "0"}), ("stage_only", {"SMFV_TILED_ABLATE": "1"}),
-                  ("compute_only", {"SMFV_TILED_ABLATE": "2"}), ("untiled", {"LAB_TILES": "off"})):
+for mode, env in (("pipe", {"SMFV_TILED_ABLATE": "0", "LAB_TILES": "force"}),
+                  ("pipe_contig", {"SMFV_TILED_ABLATE": "0", "SMFV_TILE_ORDER": "0", "LAB_TILES": "force"}),
+                  ("pipe_nocompute", {"SMFV_TILED_ABLATE": "5", "LAB_TILES": "force"}),
+                  ("pipe_nocompute_contig", {"SMFV_TILED_ABLATE": "5", "SMFV_TILE_ORDER": "0", "LAB_TILES": "force"}),
+                  ("pipe_noprefetch", {"SMFV_TILED_ABLATE": "6", "LAB_TILES": "force"}),
+                  ("oneshot", {"SMFV_TILED_ABLATE": "1", "LAB_TILES": "force"}),
+                  ("untiled", {"LAB_TILES": "off"})):
     r = subprocess.run([sys.executable, "-c", f"ROOT={ROOT!r}; MODE={mode!r}\n" + CHILD],
                        env=dict(os.environ, **env), capture_output=True, text=True, timeout=300)
     line = [l for l in r.stdout.splitlines() if l.startswith("RESULT")]

@@ -446,6 +446,262 @@ __global__ __launch_bounds__(256) void k_rows_tiled(
     *reinterpret_cast<double2 *>(y + 16 * (par ^ 1)) = acc1;
 }
 
+// ---------------------------------------------------------------------------
+// k_rows_pipe: the production tiled kernel.  Persistent blocks (a few per
+// CU), each walking a contiguous range of tiles; tile t+1 is prefetched into
+// registers (X rows, values, local columns, and the record of tile t+2)
+// while tile t is computed from LDS, then written to LDS after a barrier
+// (register staging: ordinary loads only, so hipcc's own wait counts stay
+// exact).  Per tile the dependent global round trips (record -> union ids ->
+// X rows) are hidden behind the previous tile's compute.  LDS per block:
+// X image 32 KiB + values 8 KiB + local columns 2 KiB + 2 records 2 KiB.
+// Compute is k_rows_tiled's: 8-lane teams, conflict-free swizzled halves,
+// CSR order, separate multiply / add.
+// ---------------------------------------------------------------------------
+typedef double pipe_d2 __attribute__((ext_vector_type(2)));
+typedef unsigned pipe_u2 __attribute__((ext_vector_type(2)));
+// Registers of the tile in flight (native vector types: HIP's union-based
+// double2 in a conditionally written aggregate is demoted to scratch).
+struct PipeStage {
+    pipe_d2 x[TILE_UCAP / 16];  // 8 x 16 B of union rows (tid>>4) + 16k
+    pipe_d2 v[2];               // 4 values
+    pipe_u2 l;                  // 4 local columns (u16)
+    int rec;                    // one word of the record two tiles ahead
+};
+
+__device__ __forceinline__ void pipe_load(PipeStage &S, const int *R, const uint16_t *__restrict__ tlidx,
+                                          const double *__restrict__ tvals,
+                                          const double *__restrict__ X, int64_t ldx, int cp, int tid)
+{
+    const int noff = R[0], tn = R[1], nu = R[3], direct = R[6];
+    if (direct) return;
+    const int xr = tid >> 4, xs = tid & 15;
+    // the record stores union id u at TREC_UCOLS + (u % 16) * 8 + u / 16, so
+    // this thread's 8 ids (u = xr + 16k) are two aligned 16-byte LDS reads
+    const int4 c0 = *reinterpret_cast<const int4 *>(R + TREC_UCOLS + 8 * xr);
+    const int4 c1 = *reinterpret_cast<const int4 *>(R + TREC_UCOLS + 8 * xr + 4);
+    const int uc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+    for (int k = 0; k < TILE_UCAP / 16; ++k) {
+        const int u = xr + 16 * k;
+        if (u < nu)
+            S.x[k] = *reinterpret_cast<const pipe_d2 *>(X + (int64_t)uc[k] * ldx + cp + 2 * xs);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int e = 2 * tid + 512 * k;
+        if (e < tn) S.v[k] = *reinterpret_cast<const pipe_d2 *>(tvals + noff + e);
+    }
+    if (4 * tid < tn) S.l = *reinterpret_cast<const pipe_u2 *>(tlidx + noff + 4 * tid);
+}
+
+__device__ __forceinline__ void pipe_store(const PipeStage &S, const int *R, double *s_x, double *s_va,
+                                           uint16_t *s_li, int tid)
+{
+    const int tn = R[1], nu = R[3], direct = R[6];
+    if (direct) return;
+    const int xr = tid >> 4, xs = tid & 15;
+#pragma unroll
+    for (int k = 0; k < TILE_UCAP / 16; ++k) {
+        const int u = xr + 16 * k;
+        if (u < nu) reinterpret_cast<pipe_d2 *>(s_x)[u * (TILE_KP / 2) + xs] = S.x[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int e = 2 * tid + 512 * k;
+        if (e < tn) reinterpret_cast<pipe_d2 *>(s_va)[e / 2] = S.v[k];
+    }
+    if (4 * tid < tn) reinterpret_cast<pipe_u2 *>(s_li)[tid] = S.l;
+}
+
+// B8: 0 = batches of 4 + single tail steps, 1 = masked batches of 8,
+// 2 = software-pipelined masked batches of 4.
+// ABL (lab only): 0 production, 1 no compute, 2 no prefetch of X / CSR.
+template <int B8, int ABL>
+__global__ __launch_bounds__(256, 3) void k_rows_pipe(  // 3 waves / SIMD = the LDS limit
+    int ntiles, const int *__restrict__ rec, const uint16_t *__restrict__ tlidx,
+    const double *__restrict__ tvals, const int *__restrict__ rp, const int *__restrict__ ci,
+    const double *__restrict__ va, const double *__restrict__ X, int64_t ldx, int K,
+    double *__restrict__ Y, int64_t ldy, int interleave)
+{
+    __shared__ __attribute__((aligned(16))) double s_x[TILE_UCAP * TILE_KP];
+    __shared__ __attribute__((aligned(16))) double s_va[TILE_NCAP];
+    __shared__ __attribute__((aligned(16))) uint16_t s_li[TILE_NCAP];
+    __shared__ __attribute__((aligned(16))) int s_rec[2][TREC_WORDS];
+    // Tile order.  interleave (default): XCD x = blockIdx.x % 8 owns the
+    // tiles [ntiles*x/8, ntiles*(x+1)/8); its j-th block takes tiles
+    // first + j, first + j + nb, ... so the XCD's blocks sweep its range
+    // together and consecutive (neighbouring) tiles re-use each other's X
+    // rows from the XCD's L2.  Otherwise each block takes a contiguous run.
+    int t0, tstep, tlast;
+    {
+        const int G = gridDim.x;
+        if (interleave) {
+            const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+            const int nb = (G >> 3) + (x < (G & 7) ? 1 : 0);
+            const int first = (int)((int64_t)ntiles * x / 8), end = (int)((int64_t)ntiles * (x + 1) / 8);
+            t0 = first + j;
+            tstep = nb;
+            if (t0 >= end) return;  // block-uniform
+            tlast = t0 + ((end - 1 - t0) / nb) * nb;
+        } else {
+            const int b = xcd_remap(blockIdx.x, G);
+            t0 = (int)((int64_t)ntiles * b / G);
+            const int t1 = (int)((int64_t)ntiles * (b + 1) / G);
+            if (t0 >= t1) return;  // block-uniform
+            tstep = 1;
+            tlast = t1 - 1;
+        }
+    }
+    const int cp = blockIdx.y * TILE_KP;
+    const int tid = threadIdx.x, team = tid >> 3, tl = tid & 7, par = team & 1;
+    PipeStage S;
+    // prologue: record(t0) -> LDS; tile t0 + record(t0 + 1) -> registers -> LDS.
+    // Prefetch indices are clamped to the block's last tile (re-staging it on
+    // the final iteration) so every load is unconditional: a load-or-constant
+    // register would make hipcc drain vmcnt on the loop back-edge.
+    s_rec[0][tid] = rec[(int64_t)t0 * TREC_WORDS + tid];
+    __syncthreads();
+    if (ABL != 2) pipe_load(S, s_rec[0], tlidx, tvals, X, ldx, cp, tid);
+    S.rec = rec[(int64_t)min(t0 + tstep, tlast) * TREC_WORDS + tid];
+    if (ABL != 2) pipe_store(S, s_rec[0], s_x, s_va, s_li, tid);
+    s_rec[1][tid] = S.rec;
+    __syncthreads();
+    const double2 *sx0 = reinterpret_cast<const double2 *>(s_x) + par * 8 + tl;
+    const double2 *sx1 = reinterpret_cast<const double2 *>(s_x) + (par ^ 1) * 8 + tl;
+    for (int t = t0, it = 0; t <= tlast; t += tstep, ++it) {
+        const int cur = it & 1;
+        const int *R = s_rec[cur];
+        const int *Rn = s_rec[cur ^ 1];  // record of the next tile (or t itself, last)
+        // prefetch the next tile and the record of the one after it
+        if (ABL != 2) pipe_load(S, Rn, tlidx, tvals, X, ldx, cp, tid);
+        S.rec = rec[(int64_t)min(t + 2 * tstep, tlast) * TREC_WORDS + tid];
+        // compute tile t
+        const int nrows = R[5], direct = R[6];
+        if (team < nrows) {
+            const int row = R[TREC_ROWS + team];
+            double2 acc0 = make_double2(0.0, 0.0), acc1 = make_double2(0.0, 0.0);
+            if (!direct) {
+                const int info = R[TREC_INFO + team];
+                const int js = info & 0xFFFF, je = ABL == 1 ? js : js + (info >> 16);
+                if constexpr (B8 == 2) {
+                    // software-pipelined batches of 4: the X reads of batch i
+                    // go out together with the local columns / values of
+                    // batch i+1 (one LDS round trip per batch); the last batch
+                    // is masked (segments are padded to 8, reads stay inside
+                    // the staged arrays: jn is clamped)
+                    pipe_u2 lq = *reinterpret_cast<const pipe_u2 *>(s_li + js);
+                    pipe_d2 va0 = *reinterpret_cast<const pipe_d2 *>(s_va + js);
+                    pipe_d2 va1 = *reinterpret_cast<const pipe_d2 *>(s_va + js + 2);
+                    for (int j = js; j < je; j += 4) {
+                        const int l[4] = {(int)(lq.x & 0xFFFF), (int)(lq.x >> 16), (int)(lq.y & 0xFFFF),
+                                          (int)(lq.y >> 16)};
+                        double2 x0[4], x1[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            x0[u] = sx0[l[u] * (TILE_KP / 2)];
+                            x1[u] = sx1[l[u] * (TILE_KP / 2)];
+                        }
+                        const double v[4] = {va0.x, va0.y, va1.x, va1.y};
+                        // volatile: keeps these reads here, behind the X reads
+                        // (otherwise they are re-sunk to the next iteration's top)
+                        const int jn = min(j + 4, TILE_NCAP - 4);
+                        lq = *(const volatile __attribute__((address_space(3))) pipe_u2 *)(s_li + jn);
+                        va0 = *(const volatile __attribute__((address_space(3))) pipe_d2 *)(s_va + jn);
+                        va1 = *(const volatile __attribute__((address_space(3))) pipe_d2 *)(s_va + jn + 2);
+                        const int live = je - j;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {  // branch-free mask: keep or discard the sum
+                            const double2 n0 = VecT<2>::madd(acc0, v[u], x0[u]);
+                            const double2 n1 = VecT<2>::madd(acc1, v[u], x1[u]);
+                            const bool ok = u < live;
+                            acc0.x = ok ? n0.x : acc0.x;
+                            acc0.y = ok ? n0.y : acc0.y;
+                            acc1.x = ok ? n1.x : acc1.x;
+                            acc1.y = ok ? n1.y : acc1.y;
+                        }
+                    }
+                } else if constexpr (B8 == 0) {
+                    constexpr int U = 4;
+                    int j = js;
+                    for (; j + U <= je; j += U) {
+                        double2 x0[U], x1[U];
+                        double v[U];
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const int l = s_li[j + u];
+                            v[u] = s_va[j + u];
+                            x0[u] = sx0[l * (TILE_KP / 2)];
+                            x1[u] = sx1[l * (TILE_KP / 2)];
+                        }
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            acc0 = VecT<2>::madd(acc0, v[u], x0[u]);
+                            acc1 = VecT<2>::madd(acc1, v[u], x1[u]);
+                        }
+                    }
+                    for (; j < je; ++j) {
+                        const int l = s_li[j];
+                        const double v = s_va[j];
+                        acc0 = VecT<2>::madd(acc0, v, sx0[l * (TILE_KP / 2)]);
+                        acc1 = VecT<2>::madd(acc1, v, sx1[l * (TILE_KP / 2)]);
+                    }
+                } else {
+                    // batches of 8: the row segment starts 8-aligned and is
+                    // padded to a multiple of 8, so one b128 read brings 8 local
+                    // columns, four bring 8 values; entries past the row end
+                    // are read but not summed (the sum stays the CSR-order sum)
+                    constexpr int U = 4;
+                    for (int j = js; j < je; j += 8) {
+                        const uint4 lq = *reinterpret_cast<const uint4 *>(s_li + j);
+                        const pipe_d2 *vq = reinterpret_cast<const pipe_d2 *>(s_va + j);
+                        double v[8];
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const pipe_d2 t2 = vq[q];
+                            v[2 * q] = t2.x;
+                            v[2 * q + 1] = t2.y;
+                        }
+                        const unsigned lw[4] = {lq.x, lq.y, lq.z, lq.w};
+                        const int live = je - j;
+#pragma unroll
+                        for (int h = 0; h < 8; h += U) {  // X gathered U at a time
+                            double2 x0[U], x1[U];
+#pragma unroll
+                            for (int u = 0; u < U; ++u) {
+                                const int l = (lw[(h + u) >> 1] >> (16 * ((h + u) & 1))) & 0xFFFF;
+                                x0[u] = sx0[l * (TILE_KP / 2)];
+                                x1[u] = sx1[l * (TILE_KP / 2)];
+                            }
+#pragma unroll
+                            for (int u = 0; u < U; ++u) {
+                                if (h + u < live) {
+                                    acc0 = VecT<2>::madd(acc0, v[h + u], x0[u]);
+                                    acc1 = VecT<2>::madd(acc1, v[h + u], x1[u]);
+                                }
+                            }
+                        }
+                    }
+                }
+            } else {
+                for (int jj = rp[row]; jj < rp[row + 1]; ++jj) {
+                    const double *px = X + (int64_t)ci[jj] * ldx + cp + 2 * tl;
+                    const double v = va[jj];
+                    acc0 = VecT<2>::madd(acc0, v, *reinterpret_cast<const double2 *>(px + 16 * par));
+                    acc1 = VecT<2>::madd(acc1, v, *reinterpret_cast<const double2 *>(px + 16 * (par ^ 1)));
+                }
+            }
+            double *y = Y + (int64_t)row * ldy + cp + 2 * tl;
+            *reinterpret_cast<double2 *>(y + 16 * par) = acc0;
+            *reinterpret_cast<double2 *>(y + 16 * (par ^ 1)) = acc1;
+        }
+        __syncthreads();  // tile t's LDS image and record are no longer read
+        if (ABL != 2) pipe_store(S, Rn, s_x, s_va, s_li, tid);
+        s_rec[cur][tid] = S.rec;  // record of t+2 takes tile t's slot
+        __syncthreads();
+    }
+}
+
 // plan value binding: tile-ordered copy of A's values (pads -> 0)
 __global__ __launch_bounds__(256) void k_gather_vals(int64_t count, const int *__restrict__ tsrc,
                                                      const double *__restrict__ va,
@@ -924,7 +1180,7 @@ struct smfv_plan_s {
     int64_t union_rows = 0, tiled_nnz = 0, padded_nnz = 0;
     double reuse = 0.0;
     TileMeta *meta = nullptr;
-    int *trows = nullptr, *rbeg = nullptr, *ucols = nullptr, *tsrc = nullptr;
+    int *trows = nullptr, *rbeg = nullptr, *ucols = nullptr, *tsrc = nullptr, *rec = nullptr;
     uint16_t *tlidx = nullptr;
     double *tvals = nullptr;
     const double *bound_values = nullptr;  // d_values the tile-ordered copy came from
@@ -933,7 +1189,7 @@ struct smfv_plan_s {
     ~smfv_plan_s()
     {
         for (void *q : {(void *)meta, (void *)trows, (void *)rbeg, (void *)ucols, (void *)tsrc,
-                        (void *)tlidx, (void *)tvals, ws})
+                        (void *)rec, (void *)tlidx, (void *)tvals, ws})
             if (q) (void)hipFree(q);
     }
 };
@@ -1003,6 +1259,7 @@ SMFV_API int smfv_plan_create(smfv_plan_t *out, int variant, int m, int n, int64
                 if (!rc) rc = upload(&p->rbeg, T.rbeg, p->dev_bytes);
                 if (!rc) rc = upload(&p->ucols, T.ucols, p->dev_bytes);
                 if (!rc) rc = upload(&p->tsrc, T.tsrc, p->dev_bytes);
+                if (!rc) rc = upload(&p->rec, pack_tile_records(T), p->dev_bytes);
                 if (!rc) rc = upload(&p->tlidx, T.tlidx, p->dev_bytes);
                 if (!rc) {
                     const size_t b = std::max<size_t>((size_t)T.padded_nnz, 1) * sizeof(double);
@@ -1119,15 +1376,37 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             set_error("tiled plan: values not bound (call smfv_plan_bind_values with these d_values)");
             return SMFV_ERR_INVALID;
         }
-        static const int ablate = [] {  // lab-only A/B of the two phases
+        static const int ablate = [] {  // lab-only A/B: 0 pipelined (default), 1-3 one-shot modes
             const char *e = std::getenv("SMFV_TILED_ABLATE");
             return e ? std::atoi(e) : 0;
         }();
-        auto kern = ablate == 1 ? k_rows_tiled<1> : ablate == 2 ? k_rows_tiled<2> : k_rows_tiled<0>;
-        hipLaunchKernelGGL(kern, dim3((unsigned)plan->ntiles, (unsigned)(K / TILE_KP)),
-                           dim3(256), 0, as_stream(stream), plan->meta, plan->trows, plan->rbeg,
-                           plan->ucols, plan->tlidx, plan->tvals, d_row_ptr, d_col_idx, d_values,
-                           d_X, ldx, K, d_Y, ldy);
+        if (ablate == 0 || ablate >= 4) {
+            int dev = 0, ncu = 256;
+            if (hipGetDevice(&dev) == hipSuccess) {
+                int v = 0;
+                if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+                    ncu = v;
+            }
+            const int blocks = std::min(plan->ntiles, 3 * ncu);  // 3 x 44 KiB of LDS per CU
+            // lab: 4 masked batches of 8, 5 no compute, 6 no prefetch of X / CSR,
+            // 7 pipelined batches, 8 pipelined batches without prefetch
+            auto kern = ablate == 4 ? k_rows_pipe<1, 0> : ablate == 5 ? k_rows_pipe<0, 1>
+                      : ablate == 6 ? k_rows_pipe<0, 2> : ablate == 7 ? k_rows_pipe<2, 0>
+                      : ablate == 8 ? k_rows_pipe<2, 2> : k_rows_pipe<0, 0>;
+            static const int interleave = [] {  // lab: SMFV_TILE_ORDER=0 contiguous runs
+                const char *e = std::getenv("SMFV_TILE_ORDER");
+                return e ? std::atoi(e) : 1;
+            }();
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks, (unsigned)(K / TILE_KP)), dim3(256),
+                               0, as_stream(stream), plan->ntiles, plan->rec, plan->tlidx, plan->tvals,
+                               d_row_ptr, d_col_idx, d_values, d_X, ldx, K, d_Y, ldy, interleave);
+        } else {
+            auto kern = ablate == 2 ? k_rows_tiled<1> : ablate == 3 ? k_rows_tiled<2> : k_rows_tiled<0>;  // 1 one-shot, 2 stage only, 3 compute only
+            hipLaunchKernelGGL(kern, dim3((unsigned)plan->ntiles, (unsigned)(K / TILE_KP)),
+                               dim3(256), 0, as_stream(stream), plan->meta, plan->trows, plan->rbeg,
+                               plan->ucols, plan->tlidx, plan->tvals, d_row_ptr, d_col_idx, d_values,
+                               d_X, ldx, K, d_Y, ldy);
+        }
         SMFV_LAUNCHED();
         return SMFV_OK;
     }

@@ -14,6 +14,7 @@
 #include "smfv_plan.h"
 
 #include <algorithm>
+#include <cstring>
 
 namespace smfv {
 
@@ -143,6 +144,25 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
         A.meta.push_back(tm);
         ++tile;
     }
+}
+
+std::vector<int> pack_tile_records(const TileAnalysis &A)
+{
+    std::vector<int> rec(A.meta.size() * TREC_WORDS, 0);
+    for (size_t t = 0; t < A.meta.size(); ++t) {
+        int *r = rec.data() + t * TREC_WORDS;
+        const TileMeta &tm = A.meta[t];
+        static_assert(sizeof(TileMeta) == 8 * sizeof(int), "TileMeta is 8 words");
+        std::memcpy(r, &tm, sizeof tm);
+        for (int k = 0; k < tm.nrows; ++k) {
+            r[TREC_ROWS + k] = A.trows[tm.roff + k];
+            r[TREC_INFO + k] = A.rbeg[tm.roff + k];
+        }
+        // union id u at (u % 16) * 8 + u / 16: the staging thread for rows
+        // u = xr + 16k finds its 8 ids contiguous
+        for (int u = 0; u < tm.nu; ++u) r[TREC_UCOLS + (u % 16) * 8 + u / 16] = A.ucols[tm.uoff + u];
+    }
+    return rec;
 }
 
 }  // namespace smfv

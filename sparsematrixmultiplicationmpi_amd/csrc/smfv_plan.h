@@ -28,6 +28,17 @@ struct TileMeta {
     int32_t pad;
 };
 
+// Fixed-size tile record for the pipelined kernel: 256 int32 words = 1 KiB,
+// one word per lane of a 256-lane block, so a whole record is one coalesced
+// load.  Layout: [0..7] TileMeta, [8..39] rows, [40..71] packed row info,
+// [72..199] union column ids, id u at 72 + (u % 16) * 8 + u / 16 (each
+// staging thread's 8 ids are contiguous).
+constexpr int TREC_WORDS = 256;
+constexpr int TREC_ROWS = 8, TREC_INFO = 40, TREC_UCOLS = 72;
+static_assert(TREC_UCOLS + TILE_UCAP <= TREC_WORDS, "tile record too small");
+static_assert(TILE_UCAP == 128 && TREC_UCOLS % 4 == 0, "record union layout: 16 x 8, 16-B aligned");
+static_assert(TREC_INFO - TREC_ROWS >= TILE_MAXROWS, "tile record rows");
+
 struct TileAnalysis {
     std::vector<TileMeta> meta;
     std::vector<int> trows;        // rows of each tile (any order of the matrix rows)
@@ -48,5 +59,8 @@ struct TileAnalysis {
 // tile.  Every row lands in exactly one tile; the per-row non-zero order is
 // the CSR order, so results are unchanged.
 void analyse_tiles(int m, int n, const int *row_ptr, const int *col_idx, TileAnalysis &out);
+
+// Pack the analysis into 1 KiB records (TREC_WORDS per tile).
+std::vector<int> pack_tile_records(const TileAnalysis &A);
 
 }  // namespace smfv
