@@ -20,10 +20,12 @@ w, c = variants(A, 32, dev)
 print("RESULT " + json.dumps({"mode": MODE, "warm_us": round(w, 2), "cold_us": round(c, 2)}))
 '''
 for mode, env in (("pipe", {"SMFV_TILED_ABLATE": "0", "LAB_TILES": "force"}),
+                  ("pipe_sortindex", {"SMFV_TILED_ABLATE": "0", "SMFV_TILE_SORT": "index", "LAB_TILES": "force"}),
                   ("pipe_contig", {"SMFV_TILED_ABLATE": "0", "SMFV_TILE_ORDER": "0", "LAB_TILES": "force"}),
                   ("pipe_nocompute", {"SMFV_TILED_ABLATE": "5", "LAB_TILES": "force"}),
                   ("pipe_nocompute_contig", {"SMFV_TILED_ABLATE": "5", "SMFV_TILE_ORDER": "0", "LAB_TILES": "force"}),
                   ("pipe_noprefetch", {"SMFV_TILED_ABLATE": "6", "LAB_TILES": "force"}),
+                  ("pipe_skeleton", {"SMFV_TILED_ABLATE": "9", "LAB_TILES": "force"}),
                   ("oneshot", {"SMFV_TILED_ABLATE": "1", "LAB_TILES": "force"}),
                   ("untiled", {"LAB_TILES": "off"})):
     r = subprocess.run([sys.executable, "-c", f"ROOT={ROOT!r}; MODE={mode!r}\n" + CHILD],

@@ -516,13 +516,14 @@ __device__ __forceinline__ void pipe_store(const PipeStage &S, const int *R, dou
 
 // B8: 0 = batches of 4 + single tail steps, 1 = masked batches of 8,
 // 2 = software-pipelined masked batches of 4.
-// ABL (lab only): 0 production, 1 no compute, 2 no prefetch of X / CSR.
+// ABL (lab only): 0 production, 1 no compute, 2 no prefetch of X / CSR, 3 neither,
+// 4 production with per-wave phase timestamps into prof (scripts/micro).
 template <int B8, int ABL>
 __global__ __launch_bounds__(256, 3) void k_rows_pipe(  // 3 waves / SIMD = the LDS limit
     int ntiles, const int *__restrict__ rec, const uint16_t *__restrict__ tlidx,
     const double *__restrict__ tvals, const int *__restrict__ rp, const int *__restrict__ ci,
     const double *__restrict__ va, const double *__restrict__ X, int64_t ldx, int K,
-    double *__restrict__ Y, int64_t ldy, int interleave)
+    double *__restrict__ Y, int64_t ldy, int interleave, long long *__restrict__ prof)
 {
     __shared__ __attribute__((aligned(16))) double s_x[TILE_UCAP * TILE_KP];
     __shared__ __attribute__((aligned(16))) double s_va[TILE_NCAP];
@@ -555,6 +556,7 @@ __global__ __launch_bounds__(256, 3) void k_rows_pipe(  // 3 waves / SIMD = the 
     }
     const int cp = blockIdx.y * TILE_KP;
     const int tid = threadIdx.x, team = tid >> 3, tl = tid & 7, par = team & 1;
+    const long long wall_start = ABL == 4 ? wall_clock64() : 0;
     PipeStage S;
     // prologue: record(t0) -> LDS; tile t0 + record(t0 + 1) -> registers -> LDS.
     // Prefetch indices are clamped to the block's last tile (re-staging it on
@@ -562,19 +564,26 @@ __global__ __launch_bounds__(256, 3) void k_rows_pipe(  // 3 waves / SIMD = the 
     // register would make hipcc drain vmcnt on the loop back-edge.
     s_rec[0][tid] = rec[(int64_t)t0 * TREC_WORDS + tid];
     __syncthreads();
-    if (ABL != 2) pipe_load(S, s_rec[0], tlidx, tvals, X, ldx, cp, tid);
+    if (ABL != 2 && ABL != 3) pipe_load(S, s_rec[0], tlidx, tvals, X, ldx, cp, tid);
     S.rec = rec[(int64_t)min(t0 + tstep, tlast) * TREC_WORDS + tid];
-    if (ABL != 2) pipe_store(S, s_rec[0], s_x, s_va, s_li, tid);
+    if (ABL != 2 && ABL != 3) pipe_store(S, s_rec[0], s_x, s_va, s_li, tid);
     s_rec[1][tid] = S.rec;
     __syncthreads();
     const double2 *sx0 = reinterpret_cast<const double2 *>(s_x) + par * 8 + tl;
     const double2 *sx1 = reinterpret_cast<const double2 *>(s_x) + (par ^ 1) * 8 + tl;
+    long long *pw = nullptr;  // lab: [block][step<15][wave][4]; step 15: wall start / end
+    if constexpr (ABL == 4) {
+        pw = prof + ((int64_t)blockIdx.x * 16 * 4 + (tid >> 6)) * 4;
+        if ((tid & 63) == 0) pw[15 * 16 + 0] = wall_start;
+    }
     for (int t = t0, it = 0; t <= tlast; t += tstep, ++it) {
         const int cur = it & 1;
+        if constexpr (ABL == 4)
+            if ((tid & 63) == 0 && it < 15) pw[it * 16 + 0] = clock64();
         const int *R = s_rec[cur];
         const int *Rn = s_rec[cur ^ 1];  // record of the next tile (or t itself, last)
         // prefetch the next tile and the record of the one after it
-        if (ABL != 2) pipe_load(S, Rn, tlidx, tvals, X, ldx, cp, tid);
+        if (ABL != 2 && ABL != 3) pipe_load(S, Rn, tlidx, tvals, X, ldx, cp, tid);
         S.rec = rec[(int64_t)min(t + 2 * tstep, tlast) * TREC_WORDS + tid];
         // compute tile t
         const int nrows = R[5], direct = R[6];
@@ -583,7 +592,7 @@ __global__ __launch_bounds__(256, 3) void k_rows_pipe(  // 3 waves / SIMD = the 
             double2 acc0 = make_double2(0.0, 0.0), acc1 = make_double2(0.0, 0.0);
             if (!direct) {
                 const int info = R[TREC_INFO + team];
-                const int js = info & 0xFFFF, je = ABL == 1 ? js : js + (info >> 16);
+                const int js = info & 0xFFFF, je = (ABL == 1 || ABL == 3) ? js : js + (info >> 16);
                 if constexpr (B8 == 2) {
                     // software-pipelined batches of 4: the X reads of batch i
                     // go out together with the local columns / values of
@@ -695,11 +704,19 @@ __global__ __launch_bounds__(256, 3) void k_rows_pipe(  // 3 waves / SIMD = the 
             *reinterpret_cast<double2 *>(y + 16 * par) = acc0;
             *reinterpret_cast<double2 *>(y + 16 * (par ^ 1)) = acc1;
         }
+        if constexpr (ABL == 4)
+            if ((tid & 63) == 0 && it < 15) pw[it * 16 + 1] = clock64();
         __syncthreads();  // tile t's LDS image and record are no longer read
-        if (ABL != 2) pipe_store(S, Rn, s_x, s_va, s_li, tid);
+        if constexpr (ABL == 4)
+            if ((tid & 63) == 0 && it < 15) pw[it * 16 + 2] = clock64();
+        if (ABL != 2 && ABL != 3) pipe_store(S, Rn, s_x, s_va, s_li, tid);
         s_rec[cur][tid] = S.rec;  // record of t+2 takes tile t's slot
+        if constexpr (ABL == 4)
+            if ((tid & 63) == 0 && it < 15) pw[it * 16 + 3] = clock64();
         __syncthreads();
     }
+    if constexpr (ABL == 4)
+        if ((tid & 63) == 0) pw[15 * 16 + 1] = wall_clock64();
 }
 
 // plan value binding: tile-ordered copy of A's values (pads -> 0)
@@ -1389,17 +1406,17 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             }
             const int blocks = std::min(plan->ntiles, 3 * ncu);  // 3 x 44 KiB of LDS per CU
             // lab: 4 masked batches of 8, 5 no compute, 6 no prefetch of X / CSR,
-            // 7 pipelined batches, 8 pipelined batches without prefetch
+            // 7 pipelined batches, 8 pipelined batches without prefetch, 9 skeleton
             auto kern = ablate == 4 ? k_rows_pipe<1, 0> : ablate == 5 ? k_rows_pipe<0, 1>
                       : ablate == 6 ? k_rows_pipe<0, 2> : ablate == 7 ? k_rows_pipe<2, 0>
-                      : ablate == 8 ? k_rows_pipe<2, 2> : k_rows_pipe<0, 0>;
+                      : ablate == 8 ? k_rows_pipe<2, 2> : ablate == 9 ? k_rows_pipe<0, 3> : k_rows_pipe<0, 0>;
             static const int interleave = [] {  // lab: SMFV_TILE_ORDER=0 contiguous runs
                 const char *e = std::getenv("SMFV_TILE_ORDER");
                 return e ? std::atoi(e) : 1;
             }();
             hipLaunchKernelGGL(kern, dim3((unsigned)blocks, (unsigned)(K / TILE_KP)), dim3(256),
                                0, as_stream(stream), plan->ntiles, plan->rec, plan->tlidx, plan->tvals,
-                               d_row_ptr, d_col_idx, d_values, d_X, ldx, K, d_Y, ldy, interleave);
+                               d_row_ptr, d_col_idx, d_values, d_X, ldx, K, d_Y, ldy, interleave, nullptr);
         } else {
             auto kern = ablate == 2 ? k_rows_tiled<1> : ablate == 3 ? k_rows_tiled<2> : k_rows_tiled<0>;  // 1 one-shot, 2 stage only, 3 compute only
             hipLaunchKernelGGL(kern, dim3((unsigned)plan->ntiles, (unsigned)(K / TILE_KP)),
