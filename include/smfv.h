@@ -98,11 +98,13 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz,
 /* ---- plans: analysed once per (matrix pattern, K), executed many times --
  * The plan owns all device workspace (merge-path carries for NONZERO) and,
  * for SEQUENTIAL / ROWWISE / COLUMNWISE with K a multiple of 32, a clustered
- * row-tile analysis of the pattern (h_col_idx needed): tiles of <= 32 rows
- * grown by adjacency whose distinct X rows fit a 32 KiB LDS image, with a
- * tile-ordered copy of the values and 16-bit union positions.  The tiled
- * kernel stages each tile's X rows once and reads them from LDS -- same
- * per-row order and arithmetic, bit-identical result.  Tiling is used when
+ * row-tile analysis of the pattern (h_col_idx needed): tiles of <= 64 rows
+ * grown by adjacency whose distinct X rows (<= 255) fit a 64 KiB LDS image,
+ * with a tile-ordered copy of the values and 16-bit X-row offsets.  The tiled
+ * kernel (one warp-specialised block per CU, double-buffered LDS-DMA staging)
+ * stages each tile's X rows once and reads them from LDS -- same per-row
+ * order and arithmetic, bit-identical result; rows over a cap alone are
+ * gathered straight from X by a second launch.  Tiling is used when
  * the re-use (non-zeros per staged X row) is >= 3 or SMFV_PLAN_FORCE_TILES
  * is set.  A tiled plan must be bound to A's device values with
  * smfv_plan_bind_values (and re-bound after they change); execute checks
@@ -114,11 +116,12 @@ typedef struct smfv_plan_s *smfv_plan_t;
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
 SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, void *stream);
-/* Host-only diagnostic: run the clustered tile analysis, verify the
- * invariants the tiled kernel relies on (every row in exactly one tile, caps,
- * CSR order inside rows, union positions) and report out[0] tiles, [1]
- * staged X rows, [2] re-use, [3] direct tiles, [4] padded non-zeros,
- * [5] non-zeros in staged tiles.  No device needed. */
+/* Host-only diagnostic: run the clustered tile analysis and build the tiled
+ * kernel's plan, verify the invariants the kernel relies on (every row in
+ * exactly one tile or the direct list, caps, CSR order inside rows, union
+ * positions, pads on the zero row -- by replaying the kernel's reads) and
+ * report out[0] tiles, [1] staged X rows, [2] re-use, [3] direct rows,
+ * [4] tile entries (incl. pads), [5] non-zeros in tiles.  No device needed. */
 SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_col_idx,
                                double out[6]);
 SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int *d_col_idx,

@@ -9,7 +9,7 @@ root = sys.argv[1]
 filt = sys.argv[2] if len(sys.argv) > 2 else ""
 agg = collections.defaultdict(list)
 dur = collections.defaultdict(list)
-for f in sorted(glob.glob(f"{root}/p*/pmc_counter_collection.csv")):
+for f in sorted(glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True)):
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"]
         if filt and filt not in k:

@@ -719,15 +719,213 @@ __global__ __launch_bounds__(256, 3) void k_rows_pipe(  // 3 waves / SIMD = the 
         if ((tid & 63) == 0) pw[15 * 16 + 1] = wall_clock64();
 }
 
-// plan value binding: tile-ordered copy of A's values (pads -> 0)
+// ---------------------------------------------------------------------------
+// k_rows_ws: the production tiled kernel (K % 32 == 0, plans with re-use).
+// One persistent 1024-lane block per CU, warp-specialised:
+//  * waves 8-15 (loaders) stage tile t+1 into the other half of a
+//    double-buffered LDS image by LDS-DMA (global_load_lds_dwordx4): the
+//    tile's union of X rows (<= 255 x 256 B; image row 255 stays zero), its
+//    values and u16 X-row offsets (tile-ordered, interleaved per quad of
+//    teams, build_ws_plan) and its 1 KiB record;
+//  * waves 0-7 (compute) run 64 eight-lane teams, one row each, out of LDS:
+//    per batch of 8 entries, one b128 read of 8 offsets, four of 8 values,
+//    16 b128 X reads; the next batch's meta is read behind this batch's X.
+// One barrier per tile.  An LDS-DMA stalls its wave while the CU's vector
+// memory path drains, so compute waves never issue one.  Each row is summed
+// over its non-zeros in CSR order with separate multiply and add; pads read
+// the zero row with value -0.0, and acc + (-0.0 * +0.0) = acc exactly, so
+// the result is bit-identical to the reference loop.  Values, offsets and
+// records are read once (non-temporal); X rows are re-staged by later tiles
+// and keep the default policy.  Tile order: XCD x = blockIdx.x % 8 owns
+// tiles [ntiles*x/8, ntiles*(x+1)/8), its blocks sweep them together, so
+// neighbouring tiles re-use X rows from the XCD's L2.  gridDim.x % 8 == 0.
+// ---------------------------------------------------------------------------
+namespace ws {
+constexpr int SL_X = 0, SL_V = 256 * 256, SL_L = SL_V + WS_NCAP * 8, SL_R = SL_L + WS_NCAP * 2,
+              SLOT = SL_R + WS_LWORDS * 4;
+static_assert(2 * SLOT <= 160 * 1024, "two LDS slots must fit the CU's 160 KiB");
+static_assert(WS_NCAP % 512 == 0 && SL_V % 1024 == 0 && SL_L % 1024 == 0 && SL_R % 1024 == 0, "1 KiB DMA pieces");
+typedef double d2 __attribute__((ext_vector_type(2)));
+typedef int i4 __attribute__((ext_vector_type(4)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
+// LDS-DMA of 16 B per lane to lds_dst + 16 * lane (M0 written in the same
+// statement, MI355X guide recipe); NT: non-temporal source read.
+template <bool NT> __device__ __forceinline__ void dma16(const void *g, unsigned lds_dst)
+{
+    unsigned keep;
+    if constexpr (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
+}
+__device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+}  // namespace ws
+
+__global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, const int *__restrict__ grec,
+                                                     const int *__restrict__ lrec,
+                                                     const uint16_t *__restrict__ loff,
+                                                     const double *__restrict__ tv,
+                                                     const double *__restrict__ X, int64_t ldx,
+                                                     double *__restrict__ Y, int64_t ldy)
+{
+    using namespace ws;
+    __shared__ __attribute__((aligned(16))) char lds[2 * SLOT];
+    int t0, tstep, cnt;
+    {
+        const int nb = gridDim.x >> 3;  // blocks per XCD
+        const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+        const int first = (int)((int64_t)ntiles * x / 8), end = (int)((int64_t)ntiles * (x + 1) / 8);
+        t0 = first + j;
+        tstep = nb;
+        if (t0 >= end) return;  // block-uniform
+        cnt = (end - 1 - t0) / nb + 1;
+    }
+    const int tlast = t0 + (cnt - 1) * tstep;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int cp = blockIdx.y * TILE_KP;
+    const unsigned lds0 = (unsigned)(uintptr_t)lds;  // LDS byte address of slot 0
+    if (wv >= 8) {
+        // ---------------- loader waves ----------------
+        const int wl = wv - 8;
+        if (wl == 0 && lane < 32)  // zero row of both slots
+            reinterpret_cast<d2 *>(lds + (lane >> 4) * SLOT + WS_ZOFF)[lane & 15] = d2{0.0, 0.0};
+        i4 u0, u1;
+        int noff, tn, nu;
+        auto fetch_record = [&](int t) {
+            const int *G = grec + (int64_t)t * WS_GWORDS;
+            const i4 *gu = reinterpret_cast<const i4 *>(G + 32 * wl + 8 * (lane >> 4));
+            u0 = gu[0];
+            u1 = gu[1];
+            noff = G[WS_G_NOFF + (lane & 15)];
+            tn = G[WS_G_TN + (lane & 15)];
+            nu = G[WS_G_NU + (lane & 15)];
+        };
+        auto stage = [&](int t, int s) {
+            // hipcc does not count the asm DMAs: resolve the record registers
+            // here, so no wait it places for them lands between two DMAs
+            asm volatile("" ::"v"(u0), "v"(u1), "v"(noff), "v"(tn), "v"(nu));
+            const unsigned base = lds0 + s * SLOT;
+            const int uc[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int piece = 8 * wl + i;  // 1 KiB = union rows 4*piece .. +3
+                const int u = 4 * piece + (lane >> 4);
+                if (4 * piece < nu && u < WS_UCAP)
+                    dma16<false>(X + (int64_t)uc[i] * ldx + cp + 2 * (lane & 15), base + SL_X + piece * 1024);
+            }
+            for (int k = wl; k * 128 < tn; k += WS_LOADERS)
+                dma16<true>(tv + noff + 128 * k + 2 * lane, base + SL_V + k * 1024);
+            for (int k = wl; k * 512 < tn; k += WS_LOADERS)
+                dma16<true>(loff + noff + 512 * k + 8 * lane, base + SL_L + k * 1024);
+            if (wl == WS_LOADERS - 1) dma16<true>(lrec + (int64_t)t * WS_LWORDS + 4 * lane, base + SL_R);
+        };
+        fetch_record(t0);
+        stage(t0, 0);
+        fetch_record(min(t0 + tstep, tlast));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_lds();
+        for (int it = 0; it < cnt; ++it) {
+            const int t = t0 + it * tstep;
+            if (it + 1 < cnt) {
+                stage(t + tstep, (it & 1) ^ 1);
+                fetch_record(min(t + 2 * tstep, tlast));
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 has landed
+            barrier_lds();
+        }
+        return;
+    }
+    // ---------------- compute waves ----------------
+    const int tw = (tid >> 3) & 7, tl = tid & 7, par = tw & 1;
+    const int slot = tw * 8 + wv;
+    const int qk = tw & 3;  // position of the team in its quad
+    barrier_lds();
+    for (int it = 0; it < cnt; ++it) {
+        const char *base = lds + (it & 1) * SLOT;
+        const int *R = reinterpret_cast<const int *>(base + SL_R);
+        const int row = R[slot];
+        if (row >= 0) {
+            const int info = R[64 + slot];
+            const int js = info & 0xFFFF, nbat = (info >> 16) >> 3;
+            const u4 *Lq = reinterpret_cast<const u4 *>(base + SL_L) + js + qk;
+            const d2 *Vq = reinterpret_cast<const d2 *>(base + SL_V) + R[128 + slot] + qk;
+            const char *xb0 = base + SL_X + par * 128 + tl * 16;
+            const char *xb1 = base + SL_X + (par ^ 1) * 128 + tl * 16;
+            d2 acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0};
+            u4 ln = Lq[0];
+            d2 vn[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) vn[q] = Vq[4 * q];
+            for (int b = 0; b < nbat; ++b) {
+                const unsigned lw[4] = {ln.x, ln.y, ln.z, ln.w};
+                const double v[8] = {vn[0].x, vn[0].y, vn[1].x, vn[1].y, vn[2].x, vn[2].y, vn[3].x, vn[3].y};
+                d2 x0[8], x1[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const unsigned o = (lw[u >> 1] >> (16 * (u & 1))) & 0xFFFF;
+                    x0[u] = *reinterpret_cast<const d2 *>(xb0 + o);
+                    x1[u] = *reinterpret_cast<const d2 *>(xb1 + o);
+                }
+                // next batch's meta (the last batch re-reads itself); volatile
+                // keeps these reads here, behind this batch's X reads
+                const int bn = min(b + 1, nbat - 1);
+                ln = *(const volatile __attribute__((address_space(3))) u4 *)(Lq + 4 * bn);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    vn[q] = *(const volatile __attribute__((address_space(3))) d2 *)(Vq + 4 * (4 * bn + q));
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    acc0 = acc0 + v[u] * x0[u];
+                    acc1 = acc1 + v[u] * x1[u];
+                }
+            }
+            double *y = Y + (int64_t)row * ldy + cp + 2 * tl;
+            __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y + 16 * par));
+            __builtin_nontemporal_store(acc1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
+        }
+        barrier_lds();  // slot (it & 1) is free for tile it + 2
+    }
+}
+
+// Rows the ws plan could not tile (over a cap alone): one 8-lane team per
+// row, X gathered straight from HBM, CSR order (bit-identical).
+__global__ __launch_bounds__(256) void k_rows_list(int nrows, const int *__restrict__ rows,
+                                                   const int *__restrict__ rp, const int *__restrict__ ci,
+                                                   const double *__restrict__ va,
+                                                   const double *__restrict__ X, int64_t ldx,
+                                                   double *__restrict__ Y, int64_t ldy)
+{
+    const int team = blockIdx.x * 32 + (threadIdx.x >> 3);
+    if (team >= nrows) return;
+    const int tl = threadIdx.x & 7, par = (threadIdx.x >> 3) & 1;
+    const int cp = blockIdx.y * TILE_KP;
+    const int row = rows[team];
+    double2 acc0 = make_double2(0.0, 0.0), acc1 = make_double2(0.0, 0.0);
+    for (int jj = rp[row]; jj < rp[row + 1]; ++jj) {
+        const double *px = X + (int64_t)ci[jj] * ldx + cp + 2 * tl;
+        const double v = va[jj];
+        acc0 = VecT<2>::madd(acc0, v, *reinterpret_cast<const double2 *>(px + 16 * par));
+        acc1 = VecT<2>::madd(acc1, v, *reinterpret_cast<const double2 *>(px + 16 * (par ^ 1)));
+    }
+    double *y = Y + (int64_t)row * ldy + cp + 2 * tl;
+    *reinterpret_cast<double2 *>(y + 16 * par) = acc0;
+    *reinterpret_cast<double2 *>(y + 16 * (par ^ 1)) = acc1;
+}
+
+// plan value binding: tile-ordered copy of A's values (pads -> pad)
 __global__ __launch_bounds__(256) void k_gather_vals(int64_t count, const int *__restrict__ tsrc,
                                                      const double *__restrict__ va,
-                                                     double *__restrict__ tvals)
+                                                     double *__restrict__ tvals, double pad)
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < count) {
         const int s = tsrc[i];
-        tvals[i] = s >= 0 ? va[s] : 0.0;
+        tvals[i] = s >= 0 ? va[s] : pad;
     }
 }
 
@@ -1201,12 +1399,17 @@ struct smfv_plan_s {
     uint16_t *tlidx = nullptr;
     double *tvals = nullptr;
     const double *bound_values = nullptr;  // d_values the tile-ordered copy came from
+    // tiled kernel: 0 k_rows_ws (default), 1 k_rows_pipe (SMFV_TILE_KERNEL=pipe, A/B only)
+    int kind = 0;
+    int *ws_grec = nullptr, *ws_lrec = nullptr, *direct_rows = nullptr;
+    uint16_t *ws_loff = nullptr;
     void *ws = nullptr;
     size_t ws_bytes = 0, dev_bytes = 0;
     ~smfv_plan_s()
     {
         for (void *q : {(void *)meta, (void *)trows, (void *)rbeg, (void *)ucols, (void *)tsrc,
-                        (void *)rec, (void *)tlidx, (void *)tvals, ws})
+                        (void *)rec, (void *)tlidx, (void *)tvals, (void *)ws_grec, (void *)ws_lrec,
+                        (void *)direct_rows, (void *)ws_loff, ws})
             if (q) (void)hipFree(q);
     }
 };
@@ -1261,7 +1464,44 @@ SMFV_API int smfv_plan_create(smfv_plan_t *out, int variant, int m, int n, int64
             const double est = T.union_rows ? (double)T.tiled_nnz / (double)T.union_rows : 0.0;
             go = est >= SMFV_TILE_MIN_REUSE;
         }
-        if (go) {
+        static const bool use_pipe = [] {
+            const char *e = std::getenv("SMFV_TILE_KERNEL");
+            return e && std::string(e) == "pipe";
+        }();
+        if (go && !use_pipe) {
+            WsPlan W;
+            std::string err;
+            if (!build_ws_plan(m, n, h_row_ptr, h_col_idx, W, &err)) {
+                set_error("%s", err.c_str());
+                rc = SMFV_ERR_INVALID;
+            } else {
+                p->kind = 0;
+                p->ntiles = W.ntiles;
+                p->union_rows = W.union_rows;
+                p->tiled_nnz = W.tiled_nnz;
+                p->padded_nnz = (int64_t)W.tsrc.size();
+                p->ndirect = (int)W.direct.size();
+                p->reuse = W.union_rows ? (double)W.tiled_nnz / (double)W.union_rows : 0.0;
+                if (p->reuse >= SMFV_TILE_MIN_REUSE || (flags & SMFV_PLAN_FORCE_TILES)) {
+                    p->tiled = true;
+                    if (!rc) rc = upload(&p->ws_grec, W.grec, p->dev_bytes);
+                    if (!rc) rc = upload(&p->ws_lrec, W.lrec, p->dev_bytes);
+                    if (!rc) rc = upload(&p->ws_loff, W.loff, p->dev_bytes);
+                    if (!rc) rc = upload(&p->tsrc, W.tsrc, p->dev_bytes);
+                    if (!rc) rc = upload(&p->direct_rows, W.direct, p->dev_bytes);
+                    if (!rc) {
+                        const size_t b = std::max<size_t>((size_t)p->padded_nnz, 1) * sizeof(double);
+                        hipError_t e = hipMalloc(reinterpret_cast<void **>(&p->tvals), b);
+                        if (e != hipSuccess) {
+                            set_error("hipMalloc(tvals): %s", hipGetErrorString(e));
+                            rc = SMFV_ERR_HIP;
+                        }
+                        p->dev_bytes += b;
+                    }
+                }
+            }
+        } else if (go) {
+            p->kind = 1;
             analyse_tiles(m, n, h_row_ptr, h_col_idx, T);
             p->ntiles = (int)T.meta.size();
             p->union_rows = T.union_rows;
@@ -1337,12 +1577,21 @@ SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_
         SMFV_REQUIRE(local == tm.tn, "tile non-zero count");
     }
     for (int r = 0; r < m; ++r) SMFV_REQUIRE(seen[r], "row %d in no tile", r);
-    out[0] = (double)T.meta.size();
-    out[1] = (double)T.union_rows;
-    out[2] = T.union_rows ? (double)T.tiled_nnz / (double)T.union_rows : 0.0;
-    out[3] = (double)nd;
-    out[4] = (double)T.padded_nnz;
-    out[5] = (double)T.tiled_nnz;
+    (void)nd;
+    // the production (k_rows_ws) plan: built from the same analysis with its
+    // own caps and verified by replaying the kernel's reads
+    WsPlan W;
+    std::string err;
+    if (!build_ws_plan(m, n, h_row_ptr, h_col_idx, W, &err)) {
+        set_error("%s", err.c_str());
+        return SMFV_ERR_INVALID;
+    }
+    out[0] = (double)W.ntiles;
+    out[1] = (double)W.union_rows;
+    out[2] = W.union_rows ? (double)W.tiled_nnz / (double)W.union_rows : 0.0;
+    out[3] = (double)W.direct.size();
+    out[4] = (double)W.entries;
+    out[5] = (double)W.tiled_nnz;
     return SMFV_OK;
 }
 
@@ -1354,7 +1603,7 @@ SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, voi
     const int64_t cnt = plan->padded_nnz;
     if (cnt > 0) {
         hipLaunchKernelGGL(k_gather_vals, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0,
-                           as_stream(stream), cnt, plan->tsrc, d_values, plan->tvals);
+                           as_stream(stream), cnt, plan->tsrc, d_values, plan->tvals, -0.0);
         SMFV_LAUNCHED();
     }
     plan->bound_values = d_values;
@@ -1397,14 +1646,33 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             const char *e = std::getenv("SMFV_TILED_ABLATE");
             return e ? std::atoi(e) : 0;
         }();
-        if (ablate == 0 || ablate >= 4) {
-            int dev = 0, ncu = 256;
-            if (hipGetDevice(&dev) == hipSuccess) {
-                int v = 0;
-                if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-                    ncu = v;
+        int dev = 0, ncu = 256;
+        if (hipGetDevice(&dev) == hipSuccess) {
+            int v = 0;
+            if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+                ncu = v;
+        }
+        if (plan->kind == 0) {
+            // one persistent block per CU; a multiple of 8 (>= 8) so every XCD's tile range has blocks
+            const int blocks = std::max(8, (std::min(plan->ntiles, ncu) + 7) & ~7);
+            if (plan->ntiles > 0) {
+                hipLaunchKernelGGL(k_rows_ws, dim3((unsigned)blocks, (unsigned)(K / TILE_KP)), dim3(1024), 0,
+                                   as_stream(stream), plan->ntiles, plan->ws_grec, plan->ws_lrec, plan->ws_loff,
+                                   plan->tvals, d_X, ldx, d_Y, ldy);
+                SMFV_LAUNCHED();
             }
-            const int blocks = std::min(plan->ntiles, 3 * ncu);  // 3 x 44 KiB of LDS per CU
+            if (plan->ndirect > 0) {
+                SMFV_REQUIRE(d_col_idx, "null col_idx");
+                hipLaunchKernelGGL(k_rows_list, dim3((unsigned)((plan->ndirect + 31) / 32), (unsigned)(K / TILE_KP)),
+                                   dim3(256), 0, as_stream(stream), plan->ndirect, plan->direct_rows, d_row_ptr,
+                                   d_col_idx, d_values, d_X, ldx, d_Y, ldy);
+                SMFV_LAUNCHED();
+            }
+            return SMFV_OK;
+        }
+        if (ablate == 0 || ablate >= 4) {
+            // 3 x 44 KiB of LDS per CU; a multiple of 8 (>= 8): every XCD's tile range has blocks
+            const int blocks = std::max(8, (std::min(plan->ntiles, 3 * ncu) + 7) & ~7);
             // lab: 4 masked batches of 8, 5 no compute, 6 no prefetch of X / CSR,
             // 7 pipelined batches, 8 pipelined batches without prefetch, 9 skeleton
             auto kern = ablate == 4 ? k_rows_pipe<1, 0> : ablate == 5 ? k_rows_pipe<0, 1>

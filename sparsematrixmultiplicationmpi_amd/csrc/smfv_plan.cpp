@@ -20,7 +20,7 @@
 
 namespace smfv {
 
-void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
+void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A, const TileCaps &caps)
 {
     A = TileAnalysis();
     const int ncol = std::max(n, 1);
@@ -46,7 +46,7 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
             assigned[r] = 1;
             rows.push_back(r);
             tnnz += rp[r + 1] - rp[r];
-            tpad += (rp[r + 1] - rp[r] + 7) & ~7;
+            tpad += (rp[r + 1] - rp[r] + caps.pad - 1) & ~(caps.pad - 1);
             for (int j = rp[r]; j < rp[r + 1]; ++j) {
                 const int c = ci[j];
                 if (ustamp[c] != tile) {
@@ -61,8 +61,8 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
             }
         };
         add_row(seed);
-        const bool over = ucount > TILE_UCAP || tpad > TILE_NCAP;
-        while (!over && (int)rows.size() < TILE_MAXROWS) {
+        const bool over = ucount > caps.ucap || tpad > caps.ncap;
+        while (!over && (int)rows.size() < caps.maxrows) {
             int best = -1, best_fresh = 1 << 30;
             for (int r : cand) {
                 if (assigned[r]) continue;
@@ -96,8 +96,8 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A)
                     }
                 }
             }
-            if (ucount + best_fresh > TILE_UCAP ||
-                tpad + ((rp[best + 1] - rp[best] + 7) & ~7) > TILE_NCAP)
+            if (ucount + best_fresh > caps.ucap ||
+                tpad + ((rp[best + 1] - rp[best] + caps.pad - 1) & ~(caps.pad - 1)) > caps.ncap)
                 break;
             add_row(best);
         }
@@ -178,6 +178,183 @@ std::vector<int> pack_tile_records(const TileAnalysis &A)
         for (int u = 0; u < tm.nu; ++u) r[TREC_UCOLS + (u % 16) * 8 + u / 16] = A.ucols[tm.uoff + u];
     }
     return rec;
+}
+
+// ---------------------------------------------------------------------------
+// k_rows_ws plan
+// ---------------------------------------------------------------------------
+namespace {
+
+// Replays the reads k_rows_ws makes for every tile and checks that each row's
+// entries come out as its CSR non-zeros in order, then pads (zero row).
+bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P, std::string *err)
+{
+    auto fail = [&](const std::string &msg) {
+        if (err) *err = "ws plan: " + msg;
+        return false;
+    };
+    std::vector<char> seen((size_t)std::max(m, 1), 0);
+    for (int r : P.direct) {
+        if (r < 0 || r >= m || seen[r]) return fail("direct row out of range or repeated");
+        seen[r] = 1;
+    }
+    if ((int64_t)P.loff.size() != P.entries + WS_SLACK || P.tsrc.size() != P.loff.size())
+        return fail("entry arrays");
+    for (int t = 0; t < P.ntiles; ++t) {
+        const int *g = &P.grec[(size_t)t * WS_GWORDS];
+        const int *l = &P.lrec[(size_t)t * WS_LWORDS];
+        const int noff = g[WS_G_NOFF], tn = g[WS_G_TN], nu = g[WS_G_NU];
+        for (int q = 0; q < 16; ++q)
+            if (g[WS_G_NOFF + q] != noff || g[WS_G_TN + q] != tn || g[WS_G_NU + q] != nu)
+                return fail("record header not replicated");
+        if (noff % 32 || tn % 32 || tn <= 0 || tn > WS_NCAP || nu < 0 || nu > WS_UCAP ||
+            (int64_t)noff + tn > P.entries)
+            return fail("tile header out of range");
+        for (int q = 0; q < 256; ++q)
+            if (g[q] < 0 || g[q] >= n) return fail("union id out of range");
+        for (int e = noff; e < noff + tn; ++e)
+            if (P.loff[e] != WS_ZOFF && (P.loff[e] % 256 || P.loff[e] / 256 >= nu))
+                return fail("entry offset outside the tile's union");
+        for (int slot = 0; slot < WS_ROWS; ++slot) {
+            const int r = l[slot];
+            if (r == -1) continue;
+            if (r < 0 || r >= m || seen[r]) return fail("tile row out of range or repeated");
+            seen[r] = 1;
+            const int lb = l[64 + slot] & 0xFFFF, len = l[64 + slot] >> 16, vb = l[128 + slot];
+            const int k = (slot >> 3) & 3;
+            const int rl = rp[r + 1] - rp[r];
+            if (len % 8 || len < 8 || len < rl) return fail("row segment length");
+            for (int b = 0; b < len / 8; ++b)
+                for (int u = 0; u < 8; ++u) {
+                    const int el = 8 * b + u;
+                    const int64_t le = (int64_t)noff + (int64_t)(lb + 4 * b + k) * 8 + u;
+                    const int64_t ve = (int64_t)noff + (int64_t)(vb + 4 * (4 * b + u / 2) + k) * 2 + u % 2;
+                    if (le >= noff + tn || ve >= noff + tn) return fail("segment leaves its tile");
+                    if (el < rl) {
+                        const int j = rp[r] + el;
+                        const int u_ = P.loff[le] / 256;
+                        const int w = (u_ / 4) / 8, i = (u_ / 4) % 8, qq = u_ % 4;
+                        if (P.tsrc[ve] != j || P.loff[le] == WS_ZOFF || u_ >= nu || g[32 * w + 8 * qq + i] != ci[j])
+                            return fail("row entry is not its CSR non-zero");
+                    } else if (P.tsrc[ve] != -1 || P.loff[le] != WS_ZOFF) {
+                        return fail("pad entry does not read the zero row");
+                    }
+                }
+        }
+    }
+    for (int r = 0; r < m; ++r)
+        if (!seen[r]) return fail("row " + std::to_string(r) + " in no tile");
+    return true;
+}
+
+}  // namespace
+
+bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::string *err)
+{
+    P = WsPlan();
+    TileCaps caps;
+    caps.ucap = WS_UCAP;
+    caps.ncap = WS_NCAP - 96;  // leaves room for the quads' interleave padding
+    caps.maxrows = WS_ROWS;
+    caps.pad = 8;
+    TileAnalysis T;
+    analyse_tiles(m, n, rp, ci, T, caps);
+
+    auto len8 = [&](int r) { return std::max(8, (rp[r + 1] - rp[r] + 7) & ~7); };
+    // entries of a row set sorted by decreasing length: a quad takes 4x its first (longest) row
+    auto layout = [&](const std::vector<int> &rows) {
+        int64_t e = 0;
+        for (size_t q = 0; q < rows.size(); q += 4) e += 4 * (int64_t)len8(rows[q]);
+        return e;
+    };
+    std::vector<int> pos((size_t)std::max(n, 1), -1), ucols;
+    auto emit = [&](const std::vector<int> &R) {
+        ucols.clear();
+        for (int r : R)
+            for (int j = rp[r]; j < rp[r + 1]; ++j)
+                if (pos[ci[j]] < 0) {
+                    pos[ci[j]] = (int)ucols.size();
+                    ucols.push_back(ci[j]);
+                }
+        const int nu = (int)ucols.size();
+        const int64_t noff = P.entries;
+        std::vector<int> lrec(WS_LWORDS, 0), grec(WS_GWORDS, 0);
+        for (int s = 0; s < WS_ROWS; ++s) lrec[s] = -1;
+        int64_t e = 0;
+        for (int q = 0; 4 * q < (int)R.size(); ++q) {
+            const int w = q % 8, h = q / 8;
+            const int nb = len8(R[4 * q]) / 8;
+            const int lbase = (int)(e / 8), vbase = (int)(e / 2);
+            P.loff.resize((size_t)(noff + e + 32 * nb), (uint16_t)WS_ZOFF);
+            P.tsrc.resize((size_t)(noff + e + 32 * nb), -1);
+            for (int k = 0; k < 4 && 4 * q + k < (int)R.size(); ++k) {
+                const int r = R[4 * q + k], slot = (4 * h + k) * 8 + w;
+                for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                    const int el = j - rp[r];
+                    P.loff[(size_t)(noff + (int64_t)(lbase + 4 * (el / 8) + k) * 8 + el % 8)] =
+                        (uint16_t)(pos[ci[j]] * 256);
+                    P.tsrc[(size_t)(noff + (int64_t)(vbase + 4 * (el / 2) + k) * 2 + el % 2)] = j;
+                }
+                lrec[slot] = r;
+                lrec[64 + slot] = lbase | (len8(r) << 16);
+                lrec[128 + slot] = vbase;
+                P.tiled_nnz += rp[r + 1] - rp[r];
+            }
+            e += 32 * nb;
+        }
+        for (int w = 0; w < WS_LOADERS; ++w)
+            for (int q = 0; q < 4; ++q)
+                for (int i = 0; i < 8; ++i) {
+                    const int u = 4 * (8 * w + i) + q;
+                    grec[32 * w + 8 * q + i] = u < nu ? ucols[u] : 0;
+                }
+        for (int q = 0; q < 16; ++q) {
+            grec[WS_G_NOFF + q] = (int)noff;
+            grec[WS_G_TN + q] = (int)e;
+            grec[WS_G_NU + q] = nu;
+        }
+        for (int c : ucols) pos[c] = -1;
+        P.grec.insert(P.grec.end(), grec.begin(), grec.end());
+        P.lrec.insert(P.lrec.end(), lrec.begin(), lrec.end());
+        P.entries += e;
+        P.union_rows += nu;
+        ++P.ntiles;
+    };
+
+    std::vector<std::vector<int>> stack;
+    for (const TileMeta &tm : T.meta) {
+        std::vector<int> rows(T.trows.begin() + tm.roff, T.trows.begin() + tm.roff + tm.nrows);
+        if (tm.direct) {
+            P.direct.insert(P.direct.end(), rows.begin(), rows.end());
+            continue;
+        }
+        std::sort(rows.begin(), rows.end(), [&](int a, int b) {
+            const int la = rp[a + 1] - rp[a], lb = rp[b + 1] - rp[b];
+            return la != lb ? la > lb : a < b;
+        });
+        stack.assign(1, rows);
+        while (!stack.empty()) {
+            std::vector<int> R = std::move(stack.back());
+            stack.pop_back();
+            if (layout(R) <= WS_NCAP) {
+                emit(R);
+            } else if (R.size() == 1) {
+                P.direct.push_back(R[0]);
+            } else {
+                const size_t h = R.size() / 2;
+                stack.emplace_back(R.begin() + h, R.end());
+                stack.emplace_back(R.begin(), R.begin() + h);
+            }
+        }
+    }
+    if (P.entries + WS_SLACK > 0x7fffffff) {
+        if (err) *err = "ws plan: too many tile entries for int32 offsets";
+        return false;
+    }
+    P.loff.resize((size_t)(P.entries + WS_SLACK), (uint16_t)WS_ZOFF);
+    P.tsrc.resize((size_t)(P.entries + WS_SLACK), -1);
+    std::sort(P.direct.begin(), P.direct.end());
+    return verify_ws_plan(m, n, rp, ci, P, err);
 }
 
 }  // namespace smfv

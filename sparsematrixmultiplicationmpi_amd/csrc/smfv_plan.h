@@ -3,6 +3,7 @@
 #pragma once
 
 #include <cstdint>
+#include <string>
 #include <vector>
 
 namespace smfv {
@@ -58,9 +59,63 @@ struct TileAnalysis {
 // rows <= TILE_MAXROWS.  A row over a cap alone becomes a one-row "direct"
 // tile.  Every row lands in exactly one tile; the per-row non-zero order is
 // the CSR order, so results are unchanged.
-void analyse_tiles(int m, int n, const int *row_ptr, const int *col_idx, TileAnalysis &out);
+// Caps of one tile (defaults: the constants above).
+struct TileCaps {
+    int ucap = TILE_UCAP;        // distinct X rows
+    int ncap = TILE_NCAP;        // padded non-zeros
+    int maxrows = TILE_MAXROWS;  // rows
+    int pad = 8;                 // row segments padded to a multiple of this (power of 2)
+};
+void analyse_tiles(int m, int n, const int *row_ptr, const int *col_idx, TileAnalysis &out,
+                   const TileCaps &caps = TileCaps());
 
 // Pack the analysis into 1 KiB records (TREC_WORDS per tile).
 std::vector<int> pack_tile_records(const TileAnalysis &A);
+
+// ---------------------------------------------------------------------------
+// Plan of the warp-specialised tiled kernel k_rows_ws (one 1024-lane block
+// per CU: 8 compute waves = 64 eight-lane teams, 8 loader waves).
+// A tile holds <= WS_ROWS rows and <= WS_UCAP distinct X rows; its LDS X
+// image has 256 rows of 256 B, row WS_UCAP stays zero and is what pads read.
+// Rows are sorted by decreasing length and dealt in quads (4 teams of one
+// lane group, similar lengths); a quad's entries are interleaved in 16-byte
+// chunks (batch b of team k at chunk base + 4b + k, value pair c at chunk
+// base + 4c + k) so one meta read of a lane group touches four bank groups.
+// ---------------------------------------------------------------------------
+constexpr int WS_UCAP = 255;     // union rows per tile
+constexpr int WS_NCAP = 1536;    // LDS entries per tile (u16 offset + f64 value)
+constexpr int WS_ROWS = 64;      // rows per tile
+constexpr int WS_LOADERS = 8;    // loader waves; each stages 8 x 1 KiB of X
+constexpr int WS_ZOFF = WS_UCAP * 256;  // byte offset of the zero row
+// global record (per tile, int32): [0, 256) union ids in loader-lane order
+// (loader wave w, lane quarter q, piece i -> union id 4 * (8w + i) + q at
+// word 32w + 8q + i), then noff / tn / nu, each replicated 16x so any lane
+// reads its copy with no broadcast
+constexpr int WS_GWORDS = 320, WS_G_NOFF = 256, WS_G_TN = 272, WS_G_NU = 288;
+// LDS record (per tile, 256 int32 = 1 KiB): [0, 64) row per team slot (-1 none),
+// [64, 128) L chunk base | (padded length << 16), [128, 192) V chunk base;
+// team slot = team-in-wave * 8 + wave
+constexpr int WS_LWORDS = 256;
+constexpr int WS_SLACK = 2048;   // entries past the end (DMA over-read of the last tile)
+
+struct WsPlan {
+    int ntiles = 0;
+    std::vector<int> grec;         // WS_GWORDS per tile
+    std::vector<int> lrec;         // WS_LWORDS per tile
+    std::vector<uint16_t> loff;    // per entry: byte offset of its X row in the LDS image
+    std::vector<int> tsrc;         // per entry: CSR index of its value (-1: pad)
+    std::vector<int> direct;       // rows over a cap alone, gathered straight from X
+    int64_t union_rows = 0;        // X rows staged per 32-column panel
+    int64_t tiled_nnz = 0;         // non-zeros in tiles (not direct)
+    int64_t entries = 0;           // used length of loff / tsrc (the vectors carry WS_SLACK more)
+};
+
+// Tiles from analyse_tiles (WS caps), each packed into the interleaved
+// layout; a tile whose layout overflows WS_NCAP is split in two (by sorted
+// row order) until it fits; a single row that cannot fit becomes direct.
+// Every matrix row lands in exactly one tile or in `direct`; per-row order
+// is CSR order.  The result is verified by replaying the kernel's reads;
+// returns false (with *err) if an invariant fails.
+bool build_ws_plan(int m, int n, const int *row_ptr, const int *col_idx, WsPlan &out, std::string *err);
 
 }  // namespace smfv
