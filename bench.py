@@ -51,7 +51,10 @@ CONFIGS = {
     "cop20k_k128": ("cop20k", 128, "ROWWISE"),
     "cop20k_k1": ("cop20k", 1, "SEQUENTIAL"),
     "pow10m_k32": ("pow10m", 32, "NONZERO"),
+    # config 5: 80M x 80M, 16 nnz/row, row-partitioned over the ranks + RCCL all-gather
+    "syn80m_k32": ("syn80m", 32, "ROWWISE"),
 }
+SYN80M_ROWS = 80_000_000
 
 
 def measured_traffic(config: str, kernel: str):
@@ -147,6 +150,103 @@ def cpu_baseline(A, K: int, variant: str, budget_s: float = 20.0) -> dict:
 
 
 # ---------------------------------------------------------------------------
+def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
+    """BASELINE config 5: synthetic m x m (m = 80M), 16 uniform-random
+    columns per row (splitmix64, seed 42), X = hash integers 1..100 (seed 43).
+    Rank r generates ONLY its rows of the RowWise partition
+    (SC/...RowWise.cpp:26-29) and holds X (n x K, 20.5 GB) replicated and
+    Y (m x K) whole; a step = its row-block SpMM + the RowWise exchange as
+    one ncclAllGather of the equal Y blocks over xGMI
+    (smfv_dist_rowpart_spmm_f64).  The problem is fixed as N grows (strong
+    scaling).  Timed eagerly (RCCL inside the step)."""
+    import torch
+    import torch.distributed as dist
+    import sparsematrixmultiplicationmpi_amd as smfv
+    from sparsematrixmultiplicationmpi_amd import dist as D
+    from sparsematrixmultiplicationmpi_amd import inputs
+
+    m = n = args.rows or SYN80M_ROWS
+    first, last, _, _ = D.exchange_plan(smfv.Variant.ROWWISE, m, 0, None, K, world)
+    r0, r1 = int(first[rank]), int(last[rank]) + 1
+    t0 = time.time()
+    A = inputs.gen_random_rows(m, n, 16.0, 0.0, 16, 42, r0, r1)
+    t_gen = time.time() - t0
+    nnz_loc = A.nnz
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("gloo")
+    comm = D.Communicator.from_torch_distributed()
+    dA = smfv.DeviceCSR(A, dev)
+    del A
+    X = torch.empty((n, K), dtype=torch.float64, device=dev)
+    smfv.fill_x_hash(X, 43)
+    Y = torch.empty((m, K), dtype=torch.float64, device=dev)
+    local_plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles="off")
+    Yloc = Y[r0:r1]
+    torch.cuda.synchronize()
+
+    def timed(fn, steps):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(steps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return e0.elapsed_time(e1) / steps
+
+    step = lambda: D.dist_rowpart_spmm(comm, m, dA, X, Y, to_all=True)
+    kern = lambda: local_plan.run(X, Yloc)
+    for _ in range(args.warmup):
+        step()
+    ms_step = timed(step, args.steps)
+    ms_kern = timed(kern, args.steps)
+    t = torch.tensor([ms_step, ms_kern, float(nnz_loc)], dtype=torch.float64)
+    if world > 1:
+        tn = torch.tensor([float(nnz_loc)], dtype=torch.float64)
+        dist.all_reduce(tn)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        nnz_tot = int(tn.item())
+    else:
+        nnz_tot = nnz_loc
+    ms_step, ms_kern = float(t[0]), float(t[1])
+    mloc = r1 - r0
+    flops = 2.0 * nnz_tot * K
+    kbytes = 12 * nnz_loc + 4 * (mloc + 1) + 8 * n * K + 8 * mloc * K  # rank 0's block, X read once
+    gather_bytes = kbytes + 8 * nnz_loc * K  # random columns: one X row gathered per non-zero
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(flops / (ms_step * 1e-3) / 1e9, 3), "unit": "GFLOP/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": f"synthetic: {m}x{m}, 16 uniform-random columns/row (splitmix64 seed 42), X hash 1..100 (seed 43)",
+            "config": {"workload": f"syn80m_k32: {m}x{m} x K={K}, ROWWISE row-partitioned over {world} GPU(s)"
+                                   " + RCCL all-gather of Y", "m": m, "n": n, "nnz": nnz_tot, "K": K,
+                       "variant": "ROWWISE", "parallelism": f"rows/{world}, X replicated, Y all-gathered"},
+            "roofline": {"bound": "hbm", "achieved": round(kbytes / (ms_kern * 1e-3) / 1e9, 1),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(kbytes / (ms_kern * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": kernel_label("ROWWISE", K, {}), "algorithmic_bytes_per_launch": kbytes,
+                         "gather_model_GBps": round(gather_bytes / (ms_kern * 1e-3) / 1e9, 1),
+                         "avg_launch_ms": round(ms_kern, 4),
+                         "timing": "HIP events around eager launches (rank-local kernel alone; max over ranks)"},
+            "exchange_ms": round(ms_step - ms_kern, 4),
+            "host_generation_s": round(t_gen, 1),
+            "cpu_baseline": None,
+            "cpu_baseline_note": "none: the reference's int32 FatVector path cannot hold 80M x 32 (SURVEY 8d)",
+        }
+        print(json.dumps(out))
+    comm.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -160,6 +260,7 @@ def main() -> None:
     ap.add_argument("--tiles", default="auto", choices=["auto", "off", "force"],
                     help="row-tile LDS staging of the plan (SpmmPlan tiles=)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rows", type=int, default=0, help="syn80m_k32: matrix rows (default 80M)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -167,6 +268,9 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     kind, K, variant = CONFIGS[args.config]
     variant = args.variant or variant
+    if kind == "syn80m":
+        bench_rowpart(args, world, rank, local, K)
+        return
 
     A, label = build_matrix(kind, args.mtx)
     m, n, nnz = A.numRows, A.numCols, A.nnz

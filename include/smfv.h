@@ -231,6 +231,20 @@ SMFV_API int smfv_dist_spmm_f64(smfv_comm_t comm, int variant, int mode, int roo
                                 int K, double *d_Y, void *d_workspace, size_t workspace_bytes,
                                 void *stream);
 
+/* Row-partitioned ROWWISE (bench config 5: the matrix does not fit, or is
+ * not wanted, on every rank).  Unlike smfv_dist_spmm_f64, A is NOT
+ * replicated: rank r passes only its rows [first, last] of the RowWise
+ * partition (SC/...RowWise.cpp:26-29; smfv_dist_plan) as a local CSR
+ * (row_ptr 0-based, column ids global), X (n x K, row-major) replicated.
+ * Rank r computes its block in place at d_Y + first*K (d_Y is m x K on
+ * every rank), then the RowWise exchange: SMFV_TO_ALL all-gathers (one
+ * ncclAllGather when the blocks are equal, else all-gatherv),
+ * SMFV_TO_ROOT gathers to root (SC/...RowWise.cpp:85-87).  Collective. */
+SMFV_API int smfv_dist_rowpart_spmm_f64(smfv_comm_t comm, int mode, int root, int m, int n,
+                                        const int *d_row_ptr_local, const int *d_col_idx_local,
+                                        const double *d_values_local, const double *d_X, int K,
+                                        double *d_Y, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

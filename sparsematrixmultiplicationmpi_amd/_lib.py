@@ -82,6 +82,8 @@ _SIGS = {
     "smfv_dist_spmm_f64": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int64, _PI,
                                    c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p,
                                    c_void_p, c_size_t, c_void_p]),
+    "smfv_dist_rowpart_spmm_f64": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     # smfv_host.h
     "smfv_free": (None, [c_void_p]),
     "smfv_mtx_read": (c_int, [c_char_p, _PI, _PI, _PI64, POINTER(_PI), POINTER(_PI),

@@ -196,6 +196,41 @@ SMFV_API int smfv_dist_workspace_bytes(smfv_comm_t comm, int variant, int m, int
     return SMFV_ERR_INVALID;
 }
 
+// The one exchange step of a distributed variant: gather-to-root (Gatherv /
+// Reduce target) or all-gatherv of the ranks' blocks P.offset/P.count inside
+// xbuf; equal, back-to-back blocks go through one ncclAllGather.
+static int exchange_blocks(smfv_comm_t comm, const Plan &P, bool may_be_equal, bool to_all, int root,
+                           double *xbuf, hipStream_t st)
+{
+    const int p = comm->nranks, rank = comm->rank;
+    if (p > 1) {
+        bool equal = may_be_equal;
+        for (int r = 1; r < p && equal; ++r)
+            equal = P.count[r] == P.count[0] && P.offset[r] == P.offset[0] + r * P.count[0];
+        if (to_all && equal && P.count[0] > 0) {
+            SMFV_NCCL(ncclAllGather(xbuf + P.offset[rank], xbuf, (size_t)P.count[0], ncclDouble,
+                                    comm->nccl, st));
+        } else {
+            SMFV_NCCL(ncclGroupStart());
+            for (int r = 0; r < p; ++r) {
+                if (P.count[r] == 0) continue;
+                double *blk = xbuf + P.offset[r];
+                const size_t cnt = (size_t)P.count[r];
+                if (to_all) {
+                    SMFV_NCCL(ncclBroadcast(blk, blk, cnt, ncclDouble, r, comm->nccl, st));
+                } else if (rank == root && r != root) {
+                    SMFV_NCCL(ncclRecv(blk, cnt, ncclDouble, r, comm->nccl, st));
+                } else if (rank == r && r != root) {
+                    SMFV_NCCL(ncclSend(blk, cnt, ncclDouble, root, comm->nccl, st));
+                }
+            }
+            SMFV_NCCL(ncclGroupEnd());
+        }
+    }
+
+    return SMFV_OK;
+}
+
 SMFV_API int smfv_dist_spmm_f64(smfv_comm_t comm, int variant, int mode, int root, int m, int n,
                                 int64_t nnz, const int *h_row_ptr, const int *d_row_ptr,
                                 const int *d_col_idx, const double *d_values, const double *d_X,
@@ -247,32 +282,9 @@ SMFV_API int smfv_dist_spmm_f64(smfv_comm_t comm, int variant, int mode, int roo
     }
     if (rc) return rc;
 
-    // 2) the one exchange step: gather-to-root (Gatherv / Reduce target) or
-    //    all-gatherv; equal row blocks go through ncclAllGather
-    if (p > 1) {
-        bool equal = variant != SMFV_NONZERO;
-        for (int r = 1; r < p && equal; ++r)
-            equal = P.count[r] == P.count[0] && P.offset[r] == P.offset[0] + r * P.count[0];
-        if (to_all && equal && P.count[0] > 0) {
-            SMFV_NCCL(ncclAllGather(xbuf + P.offset[rank], xbuf, (size_t)P.count[0], ncclDouble,
-                                    comm->nccl, st));
-        } else {
-            SMFV_NCCL(ncclGroupStart());
-            for (int r = 0; r < p; ++r) {
-                if (P.count[r] == 0) continue;
-                double *blk = xbuf + P.offset[r];
-                const size_t cnt = (size_t)P.count[r];
-                if (to_all) {
-                    SMFV_NCCL(ncclBroadcast(blk, blk, cnt, ncclDouble, r, comm->nccl, st));
-                } else if (rank == root && r != root) {
-                    SMFV_NCCL(ncclRecv(blk, cnt, ncclDouble, r, comm->nccl, st));
-                } else if (rank == r && r != root) {
-                    SMFV_NCCL(ncclSend(blk, cnt, ncclDouble, root, comm->nccl, st));
-                }
-            }
-            SMFV_NCCL(ncclGroupEnd());
-        }
-    }
+    // 2) the one exchange step
+    rc = exchange_blocks(comm, P, variant != SMFV_NONZERO, to_all, root, xbuf, st);
+    if (rc) return rc;
 
     // 3) assemble Y where it is wanted
     if (!(to_all || rank == root)) return SMFV_OK;
@@ -281,6 +293,29 @@ SMFV_API int smfv_dist_spmm_f64(smfv_comm_t comm, int variant, int mode, int roo
         return smfv_combine_row_blocks_f64(m, K, p, P.first.data(), P.last.data(), xbuf, d_Y, K,
                                            stream);
     return SMFV_OK;
+}
+
+SMFV_API int smfv_dist_rowpart_spmm_f64(smfv_comm_t comm, int mode, int root, int m, int n,
+                                        const int *d_row_ptr_local, const int *d_col_idx_local,
+                                        const double *d_values_local, const double *d_X, int K,
+                                        double *d_Y, void *stream)
+{
+    SMFV_REQUIRE(comm, "null communicator");
+    SMFV_REQUIRE(mode == SMFV_TO_ROOT || mode == SMFV_TO_ALL, "bad mode %d", mode);
+    SMFV_REQUIRE(m >= 0 && n >= 0 && K >= 0, "negative size");
+    const int p = comm->nranks, rank = comm->rank;
+    SMFV_REQUIRE(root >= 0 && root < p, "bad root %d", root);
+    hipStream_t st = smfv::as_stream(stream);
+    Plan P;
+    int rc = make_plan(SMFV_ROWWISE, m, 0, nullptr, K, p, P);
+    if (rc) return rc;
+    // 1) this rank's rows [first, last] from its local CSR, in place in Y
+    const int mloc = P.last[rank] - P.first[rank] + 1;
+    rc = smfv_spmm_rowblock_f64(0, mloc, n, d_row_ptr_local, d_col_idx_local, d_values_local, d_X, K, K,
+                                d_Y + P.offset[rank], K, stream);
+    if (rc) return rc;
+    // 2) the one exchange step (all-gather of equal blocks / all-gatherv / gatherv)
+    return exchange_blocks(comm, P, true, mode == SMFV_TO_ALL, root, d_Y, st);
 }
 
 }  // extern "C"

@@ -126,3 +126,24 @@ def dist_spmm(comm: Communicator, variant: int, A: DeviceCSR, X: torch.Tensor, t
     if Y is None:
         Y = torch.zeros((A.m, K), dtype=torch.float64, device=A.device)
     return DistPlan(comm, variant, A, K, to_all, root).run(X, Y, stream)
+
+
+def dist_rowpart_spmm(comm: Communicator, m: int, A_local: DeviceCSR, X: torch.Tensor, Y: torch.Tensor,
+                      to_all: bool = True, root: int = 0, stream=None) -> torch.Tensor:
+    """Row-partitioned ROWWISE (smfv_dist_rowpart_spmm_f64): A_local holds only
+    this rank's rows of the RowWise partition of an m-row matrix (local
+    row_ptr, global column ids); X (n x K) replicated; Y (m x K) receives
+    the full result on every rank (to_all) or on root."""
+    K = X.shape[1]
+    if X.shape != (A_local.n, K) or not X.is_contiguous() or X.dtype != torch.float64:
+        raise ValueError("X must be a contiguous float64 (n, K) device tensor")
+    if Y.shape != (m, K) or not Y.is_contiguous() or Y.dtype != torch.float64:
+        raise ValueError("Y must be a contiguous float64 (m, K) device tensor")
+    first, last, _, _ = exchange_plan(Variant.ROWWISE, m, 0, None, K, comm.size)
+    if A_local.m != last[comm.rank] - first[comm.rank] + 1:
+        raise ValueError(f"rank {comm.rank}: A_local has {A_local.m} rows, its partition "
+                         f"[{first[comm.rank]}, {last[comm.rank]}] has {last[comm.rank] - first[comm.rank] + 1}")
+    rp, ci, va = A_local.ptrs()
+    call("smfv_dist_rowpart_spmm_f64", comm.handle, TO_ALL if to_all else TO_ROOT, root, m, A_local.n,
+         rp, ci, va, X.data_ptr(), K, Y.data_ptr(), stream_handle(stream))
+    return Y

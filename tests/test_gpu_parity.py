@@ -286,3 +286,21 @@ def test_tiled_plan_stats_cop20k(gpu):
     plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(A, gpu), 32)
     st = plan.stats()
     assert st["reuse"] > 1.9 and st["direct_tiles"] == 0
+
+
+def test_dist_rowpart_single_rank(gpu):
+    """Row-partitioned ROWWISE (bench config 5's path) on one rank: the local
+    CSR is the whole matrix, the exchange is a no-op; bit-identical."""
+    from sparsematrixmultiplicationmpi_amd import dist as D
+    comm = D.Communicator(0, 1, D.Communicator.new_unique_id())
+    m = 5000
+    A = smfv.gen_random_rows(m, m, 16.0, 0.0, 16, 42)
+    K = 32
+    X = np.random.default_rng(5).uniform(-1, 1, (m, K))
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    dA = smfv.DeviceCSR(A, gpu)
+    Y = torch.full((m, K), np.nan, dtype=torch.float64, device=gpu)
+    D.dist_rowpart_spmm(comm, m, dA, torch.from_numpy(X).to(gpu), Y, to_all=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref))
+    comm.close()
