@@ -722,15 +722,18 @@ __global__ __launch_bounds__(256, 3) void k_rows_pipe(  // 3 waves / SIMD = the 
 // ---------------------------------------------------------------------------
 // k_rows_ws: the production tiled kernel (K % 32 == 0, plans with re-use).
 // One persistent 1024-lane block per CU, warp-specialised:
-//  * waves 8-15 (loaders) stage tile t+1 into the other half of a
-//    double-buffered LDS image by LDS-DMA (global_load_lds_dwordx4): the
-//    tile's union of X rows (<= 255 x 256 B; image row 255 stays zero), its
-//    values and u16 X-row offsets (tile-ordered, interleaved per quad of
-//    teams, build_ws_plan) and its 1 KiB record;
+//  * waves 8-15 (loaders) stage the next work unit into the other half of a
+//    double-buffered LDS image by LDS-DMA (global_load_lds_dwordx4);
 //  * waves 0-7 (compute) run 64 eight-lane teams, one row each, out of LDS:
 //    per batch of 8 entries, one b128 read of 8 offsets, four of 8 values,
 //    16 b128 X reads; the next batch's meta is read behind this batch's X.
-// One barrier per tile.  An LDS-DMA stalls its wave while the CU's vector
+// A work unit is (tile, 32-column panel), panels innermost: a unit stages
+// the tile's union of X rows for its panel (<= 255 x 256 B; image row 255
+// stays zero) into X slot (unit & 1); the tile's values, u16 X-row offsets
+// (tile-ordered, interleaved per quad of teams, build_ws_plan) and 1 KiB
+// record are staged once per tile, with its first panel, into meta slot
+// (tile & 1) -- K = 128 reads them once, not four times.
+// One barrier per unit.  An LDS-DMA stalls its wave while the CU's vector
 // memory path drains, so compute waves never issue one.  Each row is summed
 // over its non-zeros in CSR order with separate multiply and add; pads read
 // the zero row with value -0.0, and acc + (-0.0 * +0.0) = acc exactly, so
@@ -741,10 +744,11 @@ __global__ __launch_bounds__(256, 3) void k_rows_pipe(  // 3 waves / SIMD = the 
 // neighbouring tiles re-use X rows from the XCD's L2.  gridDim.x % 8 == 0.
 // ---------------------------------------------------------------------------
 namespace ws {
-constexpr int SL_X = 0, SL_V = 256 * 256, SL_L = SL_V + WS_NCAP * 8, SL_R = SL_L + WS_NCAP * 2,
-              SLOT = SL_R + WS_LWORDS * 4;
-static_assert(2 * SLOT <= 160 * 1024, "two LDS slots must fit the CU's 160 KiB");
-static_assert(WS_NCAP % 512 == 0 && SL_V % 1024 == 0 && SL_L % 1024 == 0 && SL_R % 1024 == 0, "1 KiB DMA pieces");
+constexpr int XSLOT = 256 * 256;                                   // X image: 256 rows x 256 B
+constexpr int SL_M = 2 * XSLOT;                                    // meta slots follow the X slots
+constexpr int M_V = 0, M_L = WS_NCAP * 8, M_R = M_L + WS_NCAP * 2, MSLOT = M_R + WS_LWORDS * 4;
+static_assert(SL_M + 2 * MSLOT <= 160 * 1024, "two X and two meta slots must fit the CU's 160 KiB");
+static_assert(WS_NCAP % 512 == 0 && MSLOT % 1024 == 0 && M_L % 1024 == 0 && M_R % 1024 == 0, "1 KiB DMA pieces");
 typedef double d2 __attribute__((ext_vector_type(2)));
 typedef int i4 __attribute__((ext_vector_type(4)));
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
@@ -766,7 +770,7 @@ template <bool NT> __device__ __forceinline__ void dma16(const void *g, unsigned
 __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 }  // namespace ws
 
-__global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, const int *__restrict__ grec,
+__global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
                                                      const uint16_t *__restrict__ loff,
                                                      const double *__restrict__ tv,
@@ -774,7 +778,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, const int *__re
                                                      double *__restrict__ Y, int64_t ldy)
 {
     using namespace ws;
-    __shared__ __attribute__((aligned(16))) char lds[2 * SLOT];
+    __shared__ __attribute__((aligned(16))) char lds[SL_M + 2 * MSLOT];
     int t0, tstep, cnt;
     {
         const int nb = gridDim.x >> 3;  // blocks per XCD
@@ -786,14 +790,14 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, const int *__re
         cnt = (end - 1 - t0) / nb + 1;
     }
     const int tlast = t0 + (cnt - 1) * tstep;
+    const int nunits = cnt * npanel;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int cp = blockIdx.y * TILE_KP;
-    const unsigned lds0 = (unsigned)(uintptr_t)lds;  // LDS byte address of slot 0
+    const unsigned lds0 = (unsigned)(uintptr_t)lds;  // LDS byte address of the block's image
     if (wv >= 8) {
         // ---------------- loader waves ----------------
         const int wl = wv - 8;
-        if (wl == 0 && lane < 32)  // zero row of both slots
-            reinterpret_cast<d2 *>(lds + (lane >> 4) * SLOT + WS_ZOFF)[lane & 15] = d2{0.0, 0.0};
+        if (wl == 0 && lane < 32)  // zero row of both X slots
+            reinterpret_cast<d2 *>(lds + (lane >> 4) * XSLOT + WS_ZOFF)[lane & 15] = d2{0.0, 0.0};
         i4 u0, u1;
         int noff, tn, nu;
         auto fetch_record = [&](int t) {
@@ -805,37 +809,47 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, const int *__re
             tn = G[WS_G_TN + (lane & 15)];
             nu = G[WS_G_NU + (lane & 15)];
         };
-        auto stage = [&](int t, int s) {
+        // stage unit (tile t, panel p): X rows into X slot xs, and (first panel) the meta into slot ms
+        auto stage = [&](int t, int p, int xs, int ms) {
             // hipcc does not count the asm DMAs: resolve the record registers
             // here, so no wait it places for them lands between two DMAs
             asm volatile("" ::"v"(u0), "v"(u1), "v"(noff), "v"(tn), "v"(nu));
-            const unsigned base = lds0 + s * SLOT;
+            const unsigned xb = lds0 + xs * XSLOT;
             const int uc[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+            const int cp = p * TILE_KP;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int piece = 8 * wl + i;  // 1 KiB = union rows 4*piece .. +3
                 const int u = 4 * piece + (lane >> 4);
                 if (4 * piece < nu && u < WS_UCAP)
-                    dma16<false>(X + (int64_t)uc[i] * ldx + cp + 2 * (lane & 15), base + SL_X + piece * 1024);
+                    dma16<false>(X + (int64_t)uc[i] * ldx + cp + 2 * (lane & 15), xb + piece * 1024);
             }
-            for (int k = wl; k * 128 < tn; k += WS_LOADERS)
-                dma16<true>(tv + noff + 128 * k + 2 * lane, base + SL_V + k * 1024);
-            for (int k = wl; k * 512 < tn; k += WS_LOADERS)
-                dma16<true>(loff + noff + 512 * k + 8 * lane, base + SL_L + k * 1024);
-            if (wl == WS_LOADERS - 1) dma16<true>(lrec + (int64_t)t * WS_LWORDS + 4 * lane, base + SL_R);
+            if (p == 0) {
+                const unsigned mb = lds0 + SL_M + ms * MSLOT;
+                for (int k = wl; k * 128 < tn; k += WS_LOADERS)
+                    dma16<true>(tv + noff + 128 * k + 2 * lane, mb + M_V + k * 1024);
+                for (int k = wl; k * 512 < tn; k += WS_LOADERS)
+                    dma16<true>(loff + noff + 512 * k + 8 * lane, mb + M_L + k * 1024);
+                if (wl == WS_LOADERS - 1) dma16<true>(lrec + (int64_t)t * WS_LWORDS + 4 * lane, mb + M_R);
+            }
         };
+        // unit u = (tile index it, panel p); the record registers hold the
+        // tile being staged until its last panel is issued, then the next one
         fetch_record(t0);
-        stage(t0, 0);
-        fetch_record(min(t0 + tstep, tlast));
+        stage(t0, 0, 0, 0);
+        if (npanel == 1) fetch_record(min(t0 + tstep, tlast));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         barrier_lds();
-        for (int it = 0; it < cnt; ++it) {
-            const int t = t0 + it * tstep;
-            if (it + 1 < cnt) {
-                stage(t + tstep, (it & 1) ^ 1);
-                fetch_record(min(t + 2 * tstep, tlast));
+        int it = 0, p = 0;  // unit u + 1 to stage
+        if (++p == npanel) p = 0, ++it;
+        for (int u = 0; u < nunits; ++u) {
+            if (u + 1 < nunits) {
+                const int t = t0 + it * tstep;
+                stage(t, p, (u + 1) & 1, it & 1);
+                if (p == npanel - 1) fetch_record(min(t + tstep, tlast));
+                if (++p == npanel) p = 0, ++it;
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile t+1 has landed
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // unit u+1 has landed
             barrier_lds();
         }
         return;
@@ -845,17 +859,19 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, const int *__re
     const int slot = tw * 8 + wv;
     const int qk = tw & 3;  // position of the team in its quad
     barrier_lds();
-    for (int it = 0; it < cnt; ++it) {
-        const char *base = lds + (it & 1) * SLOT;
-        const int *R = reinterpret_cast<const int *>(base + SL_R);
+    int it = 0, p = 0;
+    for (int u = 0; u < nunits; ++u) {
+        const char *xbase = lds + (u & 1) * XSLOT;
+        const char *mbase = lds + SL_M + (it & 1) * MSLOT;
+        const int *R = reinterpret_cast<const int *>(mbase + M_R);
         const int row = R[slot];
         if (row >= 0) {
             const int info = R[64 + slot];
             const int js = info & 0xFFFF, nbat = (info >> 16) >> 3;
-            const u4 *Lq = reinterpret_cast<const u4 *>(base + SL_L) + js + qk;
-            const d2 *Vq = reinterpret_cast<const d2 *>(base + SL_V) + R[128 + slot] + qk;
-            const char *xb0 = base + SL_X + par * 128 + tl * 16;
-            const char *xb1 = base + SL_X + (par ^ 1) * 128 + tl * 16;
+            const u4 *Lq = reinterpret_cast<const u4 *>(mbase + M_L) + js + qk;
+            const d2 *Vq = reinterpret_cast<const d2 *>(mbase + M_V) + R[128 + slot] + qk;
+            const char *xb0 = xbase + par * 128 + tl * 16;
+            const char *xb1 = xbase + (par ^ 1) * 128 + tl * 16;
             d2 acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0};
             u4 ln = Lq[0];
             d2 vn[4];
@@ -866,10 +882,10 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, const int *__re
                 const double v[8] = {vn[0].x, vn[0].y, vn[1].x, vn[1].y, vn[2].x, vn[2].y, vn[3].x, vn[3].y};
                 d2 x0[8], x1[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const unsigned o = (lw[u >> 1] >> (16 * (u & 1))) & 0xFFFF;
-                    x0[u] = *reinterpret_cast<const d2 *>(xb0 + o);
-                    x1[u] = *reinterpret_cast<const d2 *>(xb1 + o);
+                for (int k = 0; k < 8; ++k) {
+                    const unsigned o = (lw[k >> 1] >> (16 * (k & 1))) & 0xFFFF;
+                    x0[k] = *reinterpret_cast<const d2 *>(xb0 + o);
+                    x1[k] = *reinterpret_cast<const d2 *>(xb1 + o);
                 }
                 // next batch's meta (the last batch re-reads itself); volatile
                 // keeps these reads here, behind this batch's X reads
@@ -879,16 +895,17 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, const int *__re
                 for (int q = 0; q < 4; ++q)
                     vn[q] = *(const volatile __attribute__((address_space(3))) d2 *)(Vq + 4 * (4 * bn + q));
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    acc0 = acc0 + v[u] * x0[u];
-                    acc1 = acc1 + v[u] * x1[u];
+                for (int k = 0; k < 8; ++k) {
+                    acc0 = acc0 + v[k] * x0[k];
+                    acc1 = acc1 + v[k] * x1[k];
                 }
             }
-            double *y = Y + (int64_t)row * ldy + cp + 2 * tl;
+            double *y = Y + (int64_t)row * ldy + p * TILE_KP + 2 * tl;
             __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y + 16 * par));
             __builtin_nontemporal_store(acc1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
         }
-        barrier_lds();  // slot (it & 1) is free for tile it + 2
+        if (++p == npanel) p = 0, ++it;
+        barrier_lds();  // X slot (u & 1) is free for unit u + 2, meta slot for tile it + 1
     }
 }
 
@@ -1656,9 +1673,9 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             // one persistent block per CU; a multiple of 8 (>= 8) so every XCD's tile range has blocks
             const int blocks = std::max(8, (std::min(plan->ntiles, ncu) + 7) & ~7);
             if (plan->ntiles > 0) {
-                hipLaunchKernelGGL(k_rows_ws, dim3((unsigned)blocks, (unsigned)(K / TILE_KP)), dim3(1024), 0,
-                                   as_stream(stream), plan->ntiles, plan->ws_grec, plan->ws_lrec, plan->ws_loff,
-                                   plan->tvals, d_X, ldx, d_Y, ldy);
+                hipLaunchKernelGGL(k_rows_ws, dim3((unsigned)blocks), dim3(1024), 0, as_stream(stream), plan->ntiles,
+                                   K / TILE_KP, plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx,
+                                   d_Y, ldy);
                 SMFV_LAUNCHED();
             }
             if (plan->ndirect > 0) {

@@ -304,3 +304,21 @@ def test_dist_rowpart_single_rank(gpu):
     torch.cuda.synchronize()
     assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref))
     comm.close()
+
+
+@pytest.mark.parametrize("name", ["sym5.mtx", "pat4x6.mtx", "empty7x5.mtx"])
+@pytest.mark.parametrize("K", [32, 64])
+def test_tiled_plan_tiny(gpu, name, K):
+    """Forced tiles on matrices with fewer tiles than XCDs (one tile, empty
+    rows, a duplicate entry): every row is still computed, bit-identical."""
+    import os
+    A = smfv.readMatrixMarketFile(os.path.join(os.path.dirname(__file__), "golden", name))
+    X = np.random.default_rng(K).uniform(-1, 1, (A.numCols, K))
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    dA = smfv.DeviceCSR(A, gpu)
+    plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles="force")
+    assert plan.stats()["tiled"]
+    Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+    plan.run(torch.from_numpy(X).to(gpu), Y)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref))
