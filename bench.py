@@ -149,6 +149,33 @@ def cpu_baseline(A, K: int, variant: str, budget_s: float = 20.0) -> dict:
             "seconds_per_call": t}
 
 
+def vendor_leg(copies, args, timed, flops: float):
+    """rocSPARSE generic SpMM (the PETSc-block analogue, SC/main.cpp:289-402)
+    on the same resident copies, same rotation and graph timing as the
+    engine's kernel: the library line beside `value`, not part of it."""
+    import torch
+    import sparsematrixmultiplicationmpi_amd as smfv
+    try:
+        vs = torch.cuda.Stream()  # rocSPARSE launches on the stream bound at creation: capture on it
+        hs = [smfv.VendorSpmm(plan.A, dX, dY, alg=0, stream=vs) for plan, dX, dY in copies]
+        with torch.cuda.stream(vs):
+            for h in hs:
+                h.run()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=vs):
+            for i in range(args.steps):
+                hs[i % len(hs)].run()
+        g.replay()
+        torch.cuda.synchronize()
+        ms = timed(g) / args.steps
+        return {"library": "rocSPARSE rocsparse_spmm (CSR, f64, row-major, alg default)",
+                "avg_launch_ms": round(ms, 6), "GFLOPs": round(flops / (ms * 1e-3) / 1e9, 3),
+                "timing": "same copies / rotation / hipGraph replay as the engine's kernel"}
+    except Exception as e:  # a comparator must never sink the headline line
+        return {"library": "rocSPARSE", "error": repr(e)[:200]}
+
+
 # ---------------------------------------------------------------------------
 def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
     """BASELINE config 5: synthetic m x m (m = 80M), 16 uniform-random
@@ -261,6 +288,7 @@ def main() -> None:
                     help="row-tile LDS staging of the plan (SpmmPlan tiles=)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rows", type=int, default=0, help="syn80m_k32: matrix rows (default 80M)")
+    ap.add_argument("--no-vendor", action="store_true", help="skip the rocSPARSE comparator leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -351,6 +379,9 @@ def main() -> None:
 
     span_ms = timed(capture(False))
     span_ms_w = timed(capture(True))
+    vendor = None
+    if variant in ("ROWWISE", "SEQUENTIAL") and not args.no_vendor:
+        vendor = vendor_leg(copies, args, timed, 2.0 * nnz * K)
     ms_per_step = span_ms / args.steps
     kern_ms = ms_per_step  # average launch duration incl. the graph's kernel boundaries
     kern_ms_w = span_ms_w / args.steps
@@ -396,6 +427,7 @@ def main() -> None:
                      "GFLOPs": round(world * flops / (span_ms_w / args.steps * 1e-3) / 1e9, 3)},
             "effective_GFLOPs_per_gpu": round(flops / (ms_per_step * 1e-3) / 1e9, 3),
             "cpu_baseline": cpu,
+            "vendor_rocsparse": vendor,
         }
         print(json.dumps(out))
     if world > 1:

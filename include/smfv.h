@@ -245,6 +245,22 @@ SMFV_API int smfv_dist_rowpart_spmm_f64(smfv_comm_t comm, int mode, int root, in
                                         const double *d_values_local, const double *d_X, int K,
                                         double *d_Y, void *stream);
 
+/* ---- vendor-library comparator (not on the product path) ---------------
+ * Y = A * X by rocSPARSE's generic SpMM (CSR int32 / f64, row-major X and
+ * Y), the analogue of the reference's PETSc MatMatMult comparison block
+ * (SC/main.cpp:289-402).  create binds the operands, sizes and allocates the
+ * rocSPARSE buffer and runs its preprocess stage; execute runs the compute
+ * stage on the stream given at creation.  alg: 0 rocSPARSE default, 1 CSR
+ * row split, 2 CSR merge path.  rocSPARSE's summation order is its own: its
+ * result matches the reference within tolerance, not bit for bit. */
+typedef struct smfv_vendor_s *smfv_vendor_t;
+SMFV_API int smfv_vendor_spmm_create(smfv_vendor_t *handle, int alg, int m, int n, int64_t nnz,
+                                     const int *d_row_ptr, const int *d_col_idx, const double *d_values,
+                                     const double *d_X, int64_t ldx, int K, double *d_Y, int64_t ldy,
+                                     void *stream);
+SMFV_API int smfv_vendor_spmm_execute(smfv_vendor_t handle);
+SMFV_API int smfv_vendor_spmm_destroy(smfv_vendor_t handle);
+
 #ifdef __cplusplus
 }
 #endif

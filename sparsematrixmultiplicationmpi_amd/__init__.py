@@ -25,6 +25,7 @@ from .inputs import (  # noqa: F401
 from .engine import (  # noqa: F401
     DeviceCSR,
     SpmmPlan,
+    VendorSpmm,
     Variant,
     compare,
     fill_x_hash,

@@ -84,6 +84,10 @@ _SIGS = {
                                    c_void_p, c_size_t, c_void_p]),
     "smfv_dist_rowpart_spmm_f64": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                            c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "smfv_vendor_spmm_create": (c_int, [c_void_p, c_int, c_int, c_int, c_int64, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64, c_void_p]),
+    "smfv_vendor_spmm_execute": (c_int, [c_void_p]),
+    "smfv_vendor_spmm_destroy": (c_int, [c_void_p]),
     # smfv_host.h
     "smfv_free": (None, [c_void_p]),
     "smfv_mtx_read": (c_int, [c_char_p, _PI, _PI, _PI64, POINTER(_PI), POINTER(_PI),

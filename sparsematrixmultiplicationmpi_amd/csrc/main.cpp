@@ -9,9 +9,13 @@
 // (SC/scripts/get_csv_all.sh:18-48).  Every SpMM runs on the rank's MI355X
 // through libsmfv; the timed region of each call is the API end-to-end time
 // (host FatVector -> device -> kernel -> RCCL gather -> host FatVector).  The
-// PETSc comparison block (SC/main.cpp:282-402) is not part of this engine.
+// PETSc comparison block (SC/main.cpp:282-402) becomes a rocSPARSE block on
+// rank 0's GPU: operands converted / uploaded untimed, the library product
+// timed (as MatProductCreate + MatMatMult are, :345-347), result checked
+// against the serial one (:379-389).
 #include <mpi.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <iostream>
@@ -22,7 +26,10 @@
 #include "SparseMatrixFatVectorMultiplyColumnWise.h"
 #include "SparseMatrixFatVectorMultiplyNonZeroElement.h"
 #include "SparseMatrixFatVectorMultiplyRowWise.h"
+#include "smfv.h"
 #include "utils.h"
+
+#include <hip/hip_runtime.h>
 
 namespace {
 
@@ -60,6 +67,45 @@ void run_variant(const char *name, FatVector (*fn)(const SparseMatrix &, const F
         std::cout << name << ": Results are "
                   << (areMatricesEqual(serial, y, 1e-6) ? "the same!" : "different!") << std::endl;
     }
+}
+
+// SC/main.cpp:289-402 with rocSPARSE in place of PETSc (rank 0, one GPU)
+void run_vendor(const SparseMatrix &M, const FatVector &v, int k, const FatVector &serial)
+{
+    const int m = M.numRows, n = M.numCols;
+    const int64_t nnz = (int64_t)M.values.size();
+    if (m <= 0 || n <= 0 || k <= 0) return;
+    std::vector<double> flat = serialize(v), out((size_t)m * k);
+    int *rp = nullptr, *ci = nullptr;
+    double *va = nullptr, *X = nullptr, *Y = nullptr;
+    bool ok = hipMalloc(&rp, (m + 1) * sizeof(int)) == hipSuccess &&
+              hipMalloc(&ci, std::max<int64_t>(nnz, 1) * sizeof(int)) == hipSuccess &&
+              hipMalloc(&va, std::max<int64_t>(nnz, 1) * sizeof(double)) == hipSuccess &&
+              hipMalloc(&X, flat.size() * sizeof(double)) == hipSuccess &&
+              hipMalloc(&Y, out.size() * sizeof(double)) == hipSuccess;
+    ok = ok && hipMemcpy(rp, M.rowPtr.data(), (m + 1) * sizeof(int), hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(ci, M.colIndices.data(), nnz * sizeof(int), hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(va, M.values.data(), nnz * sizeof(double), hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(X, flat.data(), flat.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
+    smfv_vendor_t h = nullptr;
+    double t0 = 0, t1 = 0;
+    if (ok) {
+        t0 = MPI_Wtime();
+        ok = smfv_vendor_spmm_create(&h, 0, m, n, nnz, rp, ci, va, X, k, k, Y, k, nullptr) == SMFV_OK &&
+             smfv_vendor_spmm_execute(h) == SMFV_OK && hipDeviceSynchronize() == hipSuccess;
+        t1 = MPI_Wtime();
+    }
+    ok = ok && hipMemcpy(out.data(), Y, out.size() * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess;
+    if (h) smfv_vendor_spmm_destroy(h);
+    for (void *p : {(void *)rp, (void *)ci, (void *)va, (void *)X, (void *)Y})
+        if (p) (void)hipFree(p);
+    if (!ok) {
+        std::cerr << "rocSPARSE comparator failed: " << smfv_last_error() << std::endl;
+        return;
+    }
+    std::cout << "rocSPARSE Execution time: " << (t1 - t0) << std::endl;
+    std::cout << "rocSPARSE: Results are "
+              << (areMatricesEqual(serial, deserialize(out, m, k), 1e-6) ? "the same!" : "different!") << std::endl;
 }
 
 }  // namespace
@@ -103,6 +149,7 @@ int main(int argc, char *argv[])
     run_variant("Row-wise", sparseMatrixFatVectorMultiplyRowWise, M, v, k, serial, rank);
     run_variant("Column-wise", sparseMatrixFatVectorMultiplyColumnWise, M, v, k, serial, rank);
     run_variant("Non-zero Elements", sparseMatrixFatVectorMultiplyNonZeroElement, M, v, k, serial, rank);
+    if (rank == 0) run_vendor(M, v, k, serial);
 
     MPI_Barrier(MPI_COMM_WORLD);
     MPI_Finalize();

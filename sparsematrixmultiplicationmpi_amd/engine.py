@@ -247,3 +247,33 @@ def sparseMatrixFatVectorMultiplyColumnWise(sparseMatrix: SparseMatrix, fatVecto
 def sparseMatrixFatVectorMultiplyNonZeroElement(sparseMatrix: SparseMatrix, fatVector, vecCols: int,
                                                 comm=None) -> np.ndarray:
     return _collective(Variant.NONZERO, sparseMatrix, fatVector, vecCols, comm)
+
+
+class VendorSpmm:
+    """rocSPARSE generic SpMM on the same device operands (smfv_vendor_spmm_*):
+    the vendor-library comparator, the analogue of the reference's PETSc
+    MatMatMult block (SC/main.cpp:289-402).  Not the product path.
+    alg: 0 rocSPARSE default, 1 CSR row split, 2 CSR merge path."""
+
+    def __init__(self, A: DeviceCSR, X: torch.Tensor, Y: torch.Tensor, alg: int = 0,
+                 stream: torch.cuda.Stream | None = None):
+        K = X.shape[1]
+        ldx = _check_dense(X, A.n, K, "X")
+        ldy = _check_dense(Y, A.m, K, "Y")
+        self.A, self.X, self.Y = A, X, Y  # keep the bound operands alive
+        self._h = ctypes.c_void_p()
+        rp, ci, va = A.ptrs()
+        call("smfv_vendor_spmm_create", byref(self._h), alg, A.m, A.n, A.nnz, rp, ci, va, X.data_ptr(), ldx, K,
+             Y.data_ptr(), ldy, stream_handle(stream))
+
+    def run(self) -> torch.Tensor:
+        call("smfv_vendor_spmm_execute", self._h)
+        return self.Y
+
+    def __del__(self):
+        try:
+            if self._h:
+                call("smfv_vendor_spmm_destroy", self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass

@@ -37,6 +37,9 @@ def test_cli_stdout_contract(tmp_path):
         assert re.search(rf"^{name} Execution time: [0-9.eE+-]+$", out, re.M), name
     for name in ("Row-wise", "Column-wise", "Non-zero Elements"):
         assert f"{name}: Results are the same!" in out
+    # the PETSc block's analogue (SC/main.cpp:352,388 line shapes)
+    assert re.search(r"^rocSPARSE Execution time: [0-9.eE+-]+$", out, re.M)
+    assert "rocSPARSE: Results are the same!" in out
 
 
 def test_cli_usage_error():

@@ -322,3 +322,24 @@ def test_tiled_plan_tiny(gpu, name, K):
     plan.run(torch.from_numpy(X).to(gpu), Y)
     torch.cuda.synchronize()
     assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref))
+
+
+@pytest.mark.parametrize("alg", [0, 1, 2])
+def test_vendor_rocsparse_comparator(gpu, alg):
+    """The rocSPARSE comparator (PETSc-block analogue) agrees with the
+    reference's sequential result under the reference's own check
+    (areMatricesEqual, 1e-6 absolute, SC/utils.cpp:55) and 1e-12 relative."""
+    A = smfv.gen_fem27(3000, 12, 12, 0.8, 3)
+    K = 32
+    X = smfv.generateLargeFatVector(A.numCols, K)
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    dA = smfv.DeviceCSR(A, gpu)
+    dX = torch.from_numpy(X).to(gpu)
+    Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+    v = smfv.VendorSpmm(dA, dX, Y, alg=alg)
+    v.run()
+    torch.cuda.synchronize()
+    Yh = Y.cpu().numpy()
+    scale = oracle.spmm("sequential", A.rowPtr, A.colIndices, np.abs(A.values), np.abs(X))
+    assert np.all(np.abs(Yh - Yref) <= 1e-12 * scale + 1e-300)
+    assert np.max(np.abs(Yh - Yref)) <= 1e-6
