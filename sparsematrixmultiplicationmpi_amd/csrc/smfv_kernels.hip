@@ -744,11 +744,14 @@ __global__ __launch_bounds__(256, 3) void k_rows_pipe(  // 3 waves / SIMD = the 
 // neighbouring tiles re-use X rows from the XCD's L2.  gridDim.x % 8 == 0.
 // ---------------------------------------------------------------------------
 namespace ws {
-constexpr int XSLOT = 256 * 256;                                   // X image: 256 rows x 256 B
-constexpr int SL_M = 2 * XSLOT;                                    // meta slots follow the X slots
-constexpr int M_V = 0, M_L = WS_NCAP * 8, M_R = M_L + WS_NCAP * 2, MSLOT = M_R + WS_LWORDS * 4;
+constexpr int XSLOT = (WS_UCAP + 1) * 256;  // X image: union rows + the zero row, 256 B each
+constexpr int SL_M = 2 * XSLOT;             // meta slots follow the X slots
+// values and offsets arrive in whole 1 KiB DMA pieces (128 doubles / 512 u16)
+constexpr int M_V = 0, M_L = (WS_NCAP + 127) / 128 * 1024, M_R = M_L + (WS_NCAP + 511) / 512 * 1024,
+              MSLOT = M_R + WS_LWORDS * 4;
 static_assert(SL_M + 2 * MSLOT <= 160 * 1024, "two X and two meta slots must fit the CU's 160 KiB");
-static_assert(WS_NCAP % 512 == 0 && MSLOT % 1024 == 0 && M_L % 1024 == 0 && M_R % 1024 == 0, "1 KiB DMA pieces");
+static_assert(XSLOT % 1024 == 0 && MSLOT % 1024 == 0, "1 KiB DMA pieces");
+static_assert(WS_UCAP + 1 <= 4 * 8 * WS_LOADERS, "8 X pieces per loader wave cover the image");
 typedef double d2 __attribute__((ext_vector_type(2)));
 typedef int i4 __attribute__((ext_vector_type(4)));
 typedef unsigned u4 __attribute__((ext_vector_type(4)));

@@ -264,7 +264,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     P = WsPlan();
     TileCaps caps;
     caps.ucap = WS_UCAP;
-    caps.ncap = WS_NCAP - 96;  // leaves room for the quads' interleave padding
+    caps.ncap = WS_NCAP - 192;  // leaves room for the quads' interleave padding
     caps.maxrows = WS_ROWS;
     caps.pad = 8;
     TileAnalysis T;

@@ -76,14 +76,18 @@ std::vector<int> pack_tile_records(const TileAnalysis &A);
 // Plan of the warp-specialised tiled kernel k_rows_ws (one 1024-lane block
 // per CU: 8 compute waves = 64 eight-lane teams, 8 loader waves).
 // A tile holds <= WS_ROWS rows and <= WS_UCAP distinct X rows; its LDS X
-// image has 256 rows of 256 B, row WS_UCAP stays zero and is what pads read.
+// image has WS_UCAP + 1 rows of 256 B, row WS_UCAP stays zero and is what
+// pads read.  The caps are sized so that two X images and two meta slots
+// (values, offsets, record) fill the CU's 160 KiB, and so that the tiles of
+// the cop20k_A surrogate number <= 8 per CU (1,980 tiles: every block runs
+// 8, where 2,081 tiles of the former 255 / 1,536 caps made some run 9).
 // Rows are sorted by decreasing length and dealt in quads (4 teams of one
 // lane group, similar lengths); a quad's entries are interleaved in 16-byte
 // chunks (batch b of team k at chunk base + 4b + k, value pair c at chunk
 // base + 4c + k) so one meta read of a lane group touches four bank groups.
 // ---------------------------------------------------------------------------
-constexpr int WS_UCAP = 255;     // union rows per tile
-constexpr int WS_NCAP = 1536;    // LDS entries per tile (u16 offset + f64 value)
+constexpr int WS_UCAP = 239;     // union rows per tile
+constexpr int WS_NCAP = 1792;    // LDS entries per tile (u16 offset + f64 value)
 constexpr int WS_ROWS = 64;      // rows per tile
 constexpr int WS_LOADERS = 8;    // loader waves; each stages 8 x 1 KiB of X
 constexpr int WS_ZOFF = WS_UCAP * 256;  // byte offset of the zero row
