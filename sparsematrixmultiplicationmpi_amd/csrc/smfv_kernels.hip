@@ -798,6 +798,9 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
     const unsigned lds0 = (unsigned)(uintptr_t)lds;  // LDS byte address of the block's image
     if (wv >= 8) {
         // ---------------- loader waves ----------------
+        // loaders win instruction arbitration on their SIMD: a DMA issued
+        // late stretches the whole unit (30.1 -> 28.0 us on the surrogate)
+        __builtin_amdgcn_s_setprio(3);
         const int wl = wv - 8;
         if (wl == 0 && lane < 32)  // zero row of both X slots
             reinterpret_cast<d2 *>(lds + (lane >> 4) * XSLOT + WS_ZOFF)[lane & 15] = d2{0.0, 0.0};
@@ -820,6 +823,14 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
             const unsigned xb = lds0 + xs * XSLOT;
             const int uc[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
             const int cp = p * TILE_KP;
+            auto stage_meta = [&]() {
+                const unsigned mb = lds0 + SL_M + ms * MSLOT;
+                for (int k = wl; k * 128 < tn; k += WS_LOADERS)
+                    dma16<true>(tv + noff + 128 * k + 2 * lane, mb + M_V + k * 1024);
+                for (int k = wl; k * 512 < tn; k += WS_LOADERS)
+                    dma16<true>(loff + noff + 512 * k + 8 * lane, mb + M_L + k * 1024);
+                if (wl == WS_LOADERS - 1) dma16<true>(lrec + (int64_t)t * WS_LWORDS + 4 * lane, mb + M_R);
+            };
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int piece = 8 * wl + i;  // 1 KiB = union rows 4*piece .. +3
@@ -827,14 +838,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
                 if (4 * piece < nu && u < WS_UCAP)
                     dma16<false>(X + (int64_t)uc[i] * ldx + cp + 2 * (lane & 15), xb + piece * 1024);
             }
-            if (p == 0) {
-                const unsigned mb = lds0 + SL_M + ms * MSLOT;
-                for (int k = wl; k * 128 < tn; k += WS_LOADERS)
-                    dma16<true>(tv + noff + 128 * k + 2 * lane, mb + M_V + k * 1024);
-                for (int k = wl; k * 512 < tn; k += WS_LOADERS)
-                    dma16<true>(loff + noff + 512 * k + 8 * lane, mb + M_L + k * 1024);
-                if (wl == WS_LOADERS - 1) dma16<true>(lrec + (int64_t)t * WS_LWORDS + 4 * lane, mb + M_R);
-            }
+            if (p == 0) stage_meta();
         };
         // unit u = (tile index it, panel p); the record registers hold the
         // tile being staged until its last panel is issued, then the next one
