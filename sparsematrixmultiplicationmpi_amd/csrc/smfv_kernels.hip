@@ -773,6 +773,9 @@ template <bool NT> __device__ __forceinline__ void dma16(const void *g, unsigned
 __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 }  // namespace ws
 
+// ABL (lab A/B only, SMFV_WS_ABL): 1 staging only (no compute), 2 compute
+// only (every unit recomputes the first staged tile), 3 as 2 without Y stores
+template <int ABL>
 __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
                                                      const uint16_t *__restrict__ loff,
@@ -850,7 +853,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
         int it = 0, p = 0;  // unit u + 1 to stage
         if (++p == npanel) p = 0, ++it;
         for (int u = 0; u < nunits; ++u) {
-            if (u + 1 < nunits) {
+            if (u + 1 < nunits && ABL != 2 && ABL != 3) {
                 const int t = t0 + it * tstep;
                 stage(t, p, (u + 1) & 1, it & 1);
                 if (p == npanel - 1) fetch_record(min(t + tstep, tlast));
@@ -868,11 +871,12 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
     barrier_lds();
     int it = 0, p = 0;
     for (int u = 0; u < nunits; ++u) {
-        const char *xbase = lds + (u & 1) * XSLOT;
-        const char *mbase = lds + SL_M + (it & 1) * MSLOT;
+        // (ABL 2 / 3 recompute the prologue's unit: slot 0 is the only staged one)
+        const char *xbase = lds + (ABL >= 2 ? 0 : (u & 1)) * XSLOT;
+        const char *mbase = lds + SL_M + (ABL >= 2 ? 0 : (it & 1)) * MSLOT;
         const int *R = reinterpret_cast<const int *>(mbase + M_R);
         const int row = R[slot];
-        if (row >= 0) {
+        if (row >= 0 && ABL != 1) {
             const int info = R[64 + slot];
             const int js = info & 0xFFFF, nbat = (info >> 16) >> 3;
             const u4 *Lq = reinterpret_cast<const u4 *>(mbase + M_L) + js + qk;
@@ -880,20 +884,27 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
             const char *xb0 = xbase + par * 128 + tl * 16;
             const char *xb1 = xbase + (par ^ 1) * 128 + tl * 16;
             d2 acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0};
+            // per batch of 8 entries: 8 offsets in one b128 read, 8 values in
+            // four; X is read in halves of 4 entries, ping-pong: the reads of
+            // the next half go out before the current half is summed, so each
+            // half's LDS latency hides behind the other half's FP64 work
+            auto rdx = [&](unsigned w, d2 &a0, d2 &a1, d2 &b0, d2 &b1) {
+                a0 = *reinterpret_cast<const d2 *>(xb0 + (w & 0xFFFF));
+                a1 = *reinterpret_cast<const d2 *>(xb1 + (w & 0xFFFF));
+                b0 = *reinterpret_cast<const d2 *>(xb0 + (w >> 16));
+                b1 = *reinterpret_cast<const d2 *>(xb1 + (w >> 16));
+            };
             u4 ln = Lq[0];
             d2 vn[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) vn[q] = Vq[4 * q];
+            d2 xa0[4], xa1[4], xc0[4], xc1[4];
+            rdx(ln.x, xa0[0], xa1[0], xa0[1], xa1[1]);
+            rdx(ln.y, xa0[2], xa1[2], xa0[3], xa1[3]);
             for (int b = 0; b < nbat; ++b) {
-                const unsigned lw[4] = {ln.x, ln.y, ln.z, ln.w};
+                rdx(ln.z, xc0[0], xc1[0], xc0[1], xc1[1]);  // second half of batch b
+                rdx(ln.w, xc0[2], xc1[2], xc0[3], xc1[3]);
                 const double v[8] = {vn[0].x, vn[0].y, vn[1].x, vn[1].y, vn[2].x, vn[2].y, vn[3].x, vn[3].y};
-                d2 x0[8], x1[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const unsigned o = (lw[k >> 1] >> (16 * (k & 1))) & 0xFFFF;
-                    x0[k] = *reinterpret_cast<const d2 *>(xb0 + o);
-                    x1[k] = *reinterpret_cast<const d2 *>(xb1 + o);
-                }
                 // next batch's meta (the last batch re-reads itself); volatile
                 // keeps these reads here, behind this batch's X reads
                 const int bn = min(b + 1, nbat - 1);
@@ -902,14 +913,23 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
                 for (int q = 0; q < 4; ++q)
                     vn[q] = *(const volatile __attribute__((address_space(3))) d2 *)(Vq + 4 * (4 * bn + q));
 #pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    acc0 = acc0 + v[k] * x0[k];
-                    acc1 = acc1 + v[k] * x1[k];
+                for (int k = 0; k < 4; ++k) {
+                    acc0 = acc0 + v[k] * xa0[k];
+                    acc1 = acc1 + v[k] * xa1[k];
+                }
+                rdx(ln.x, xa0[0], xa1[0], xa0[1], xa1[1]);  // first half of batch b + 1
+                rdx(ln.y, xa0[2], xa1[2], xa0[3], xa1[3]);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    acc0 = acc0 + v[4 + k] * xc0[k];
+                    acc1 = acc1 + v[4 + k] * xc1[k];
                 }
             }
             double *y = Y + (int64_t)row * ldy + p * TILE_KP + 2 * tl;
-            __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y + 16 * par));
-            __builtin_nontemporal_store(acc1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
+            if (ABL != 3 || acc0.x != acc0.x) {
+                __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y + 16 * par));
+                __builtin_nontemporal_store(acc1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
+            }
         }
         if (++p == npanel) p = 0, ++it;
         barrier_lds();  // X slot (u & 1) is free for unit u + 2, meta slot for tile it + 1
@@ -1680,7 +1700,11 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             // one persistent block per CU; a multiple of 8 (>= 8) so every XCD's tile range has blocks
             const int blocks = std::max(8, (std::min(plan->ntiles, ncu) + 7) & ~7);
             if (plan->ntiles > 0) {
-                hipLaunchKernelGGL(k_rows_ws, dim3((unsigned)blocks), dim3(1024), 0, as_stream(stream), plan->ntiles,
+                static const int abl = [] {
+                    const char *e = std::getenv("SMFV_WS_ABL");
+                    return e ? std::atoi(e) : 0;
+                }();
+                hipLaunchKernelGGL(abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3> : k_rows_ws<0>, dim3((unsigned)blocks), dim3(1024), 0, as_stream(stream), plan->ntiles,
                                    K / TILE_KP, plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx,
                                    d_Y, ldy);
                 SMFV_LAUNCHED();
