@@ -61,6 +61,97 @@ template <class F> void parallel_rows(int64_t begin, int64_t end, F f)
     for (auto &x : th) x.join();
 }
 
+// Parses the entry lines of [p, end) in parallel (see smfv_mtx_read).  True
+// when every line of the region holds exactly one valid entry and there are
+// exactly nz of them; rows / ent then hold them in file order (mirrored
+// entries right after their source, as the sequential reader stores them).
+bool parse_entries_parallel(const char *p, const char *end, long long m, long long n, long long nz, bool sym,
+                            bool pat, std::vector<int> &rows, std::vector<std::pair<int, double>> &ent, int64_t &t)
+{
+    const int nt = nthreads_for(end - p);
+    if (nt == 1 || nz == 0) return false;
+    // chunk boundaries at line starts
+    std::vector<const char *> cut(nt + 1, end);
+    cut[0] = p;
+    for (int k = 1; k < nt; ++k) {
+        const char *q = p + (end - p) * k / nt;
+        if (q < cut[k - 1]) q = cut[k - 1];
+        while (q < end && q[-1] != '\n') ++q;
+        cut[k] = q;
+    }
+    // one line -> one entry: parse into per-thread buffers
+    struct Part {
+        std::vector<int> r;
+        std::vector<std::pair<int, double>> e;
+        bool ok = true;
+    };
+    std::vector<Part> part(nt);
+    auto work = [&](int k) {
+        Part &P = part[k];
+        const char *q = cut[k], *qe = cut[k + 1];
+        while (q < qe) {
+            const char *le = static_cast<const char *>(std::memchr(q, '\n', qe - q));
+            if (!le) le = qe;
+            const char *a = q;
+            while (a < le && (*a == ' ' || *a == '\t' || *a == '\r')) ++a;
+            if (a == le) {  // blank line: the sequential reader would skip it too
+                q = le + 1;
+                continue;
+            }
+            char *x;
+            const long r = std::strtol(a, &x, 10);
+            if (x == a) { P.ok = false; return; }
+            const char *b = x;
+            const long c = std::strtol(b, &x, 10);
+            if (x == b) { P.ok = false; return; }
+            double v = 1.0;
+            if (!pat) {
+                const char *d = x;
+                v = std::strtod(d, &x);
+                if (x == d) { P.ok = false; return; }
+            }
+            for (const char *z = x; z < le; ++z)  // nothing else on the line
+                if (!(*z == ' ' || *z == '\t' || *z == '\r')) { P.ok = false; return; }
+            if (r < 1 || r > m || c < 1 || c > n || (sym && r != c && c > m)) { P.ok = false; return; }
+            P.r.push_back((int)(r - 1));
+            P.e.push_back({(int)(c - 1), v});
+            if (sym && r != c) {
+                P.r.push_back((int)(c - 1));
+                P.e.push_back({(int)(r - 1), v});
+            }
+            q = le + 1;
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int k = 0; k < nt; ++k) th.emplace_back(work, k);
+        for (auto &x : th) x.join();
+    }
+    int64_t total = 0, entries = 0;
+    for (const Part &P : part) {
+        if (!P.ok) return false;
+        total += (int64_t)P.r.size();
+    }
+    // the file's entry count (a mirrored pair counts once)
+    for (const Part &P : part)
+        for (size_t i = 0; i < P.r.size(); ++i) {
+            ++entries;
+            if (sym && P.r[i] != P.e[i].first) ++i;  // skip the mirror
+        }
+    if (entries != nz || total > (int64_t)rows.size()) return false;
+    std::vector<int64_t> off(nt + 1, 0);
+    for (int k = 0; k < nt; ++k) off[k + 1] = off[k] + (int64_t)part[k].r.size();
+    std::vector<std::thread> th;
+    for (int k = 0; k < nt; ++k)
+        th.emplace_back([&, k] {
+            std::copy(part[k].r.begin(), part[k].r.end(), rows.begin() + off[k]);
+            std::copy(part[k].e.begin(), part[k].e.end(), ent.begin() + off[k]);
+        });
+    for (auto &x : th) x.join();
+    t = total;
+    return true;
+}
+
 template <class T> T *xmalloc(size_t count)
 {
     return static_cast<T *>(std::malloc(sizeof(T) * (count ? count : 1)));
@@ -156,6 +247,14 @@ SMFV_API int smfv_mtx_read(const char *path, int *out_m, int *out_n, int64_t *ou
     std::vector<std::pair<int, double>> ent((size_t)cap);
     const char *p = buf.c_str() + std::min(pos, buf.size());
     int64_t t = 0;
+    // Parallel parse (one entry per line, the layout every writer uses): the
+    // data region is cut at line starts into one chunk per thread, each chunk
+    // counted and parsed on its own, results placed by a prefix sum.  Any
+    // chunk that does not parse cleanly, or a total other than nz, falls back
+    // to the sequential token reader below (the reference's semantics: nz
+    // entries, whitespace-separated, the rest of the file ignored).
+    if (parse_entries_parallel(p, buf.c_str() + buf.size(), m, n, nz, sym, pat, rows, ent, t)) goto assemble;
+    t = 0;
     for (long long i = 0; i < nz; ++i) {
         char *endp;
         errno = 0;
@@ -186,6 +285,7 @@ SMFV_API int smfv_mtx_read(const char *path, int *out_m, int *out_n, int64_t *ou
             }
         }
     }
+assemble:
     {
         int *rp = xmalloc<int>((size_t)m + 1);
         int *ci = xmalloc<int>((size_t)t);
@@ -210,13 +310,16 @@ SMFV_API int smfv_mtx_read(const char *path, int *out_m, int *out_n, int64_t *ou
         std::vector<int64_t> fill(cnt.begin(), cnt.end() - 1);
         std::vector<std::pair<int, double>> sorted((size_t)t);
         for (int64_t i = 0; i < t; ++i) sorted[fill[rows[i]]++] = ent[i];
-        for (long long i = 0; i < m; ++i)  // per-row sort by (col, value) (utils.cpp:156-159)
-            std::sort(sorted.begin() + cnt[i], sorted.begin() + cnt[i + 1]);
+        parallel_rows(0, m, [&](int64_t a, int64_t b) {  // per-row sort by (col, value) (utils.cpp:156-159)
+            for (int64_t i = a; i < b; ++i) std::sort(sorted.begin() + cnt[i], sorted.begin() + cnt[i + 1]);
+        });
         for (long long i = 0; i <= m; ++i) rp[i] = (int)cnt[i];
-        for (int64_t i = 0; i < t; ++i) {
-            ci[i] = sorted[i].first;
-            va[i] = sorted[i].second;
-        }
+        parallel_rows(0, t, [&](int64_t a, int64_t b) {
+            for (int64_t i = a; i < b; ++i) {
+                ci[i] = sorted[i].first;
+                va[i] = sorted[i].second;
+            }
+        });
         *out_m = (int)m;
         *out_n = (int)n;
         *out_nnz = t;

@@ -214,3 +214,27 @@ def test_tile_analysis_invariants_and_reuse():
     assert _analyse(A)[0] >= 1
     A = smfv.readMatrixMarketFile(os.path.join(GOLDEN, "empty7x5.mtx"))
     assert _analyse(A)[0] >= 1
+
+
+def test_mtx_reader_parallel_and_fallback(tmp_path):
+    """The parallel Matrix Market parse (one entry per line, files > 64 KiB)
+    gives the same CSR as the sequential token reader, and files it cannot
+    cut by lines (an entry split over lines, extra trailing entries) fall
+    back to the sequential reader's semantics (SC/utils.cpp:116-153)."""
+    A = smfv.gen_random_rows(3000, 2500, 6, 2.0, 200, 9)
+    p1 = tmp_path / "a.mtx"
+    smfv.writeMatrixMarketFile(str(p1), A)
+    assert p1.stat().st_size > 65536
+    B = smfv.readMatrixMarketFile(str(p1))
+    assert np.array_equal(A.rowPtr, B.rowPtr) and np.array_equal(A.colIndices, B.colIndices)
+    assert np.array_equal(A.values.view(np.uint64), B.values.view(np.uint64))
+    lines = p1.read_text().splitlines()
+    hdr, body = lines[:2], lines[2:]
+    # first entry split over two lines + two junk entries past nz
+    r, c, v = body[0].split()
+    odd = hdr + [f"{r} {c}", v] + body[1:] + ["1 1 5.0", "2 2 6.0"]
+    p2 = tmp_path / "b.mtx"
+    p2.write_text("\n".join(odd) + "\n")
+    C = smfv.readMatrixMarketFile(str(p2))
+    assert np.array_equal(A.rowPtr, C.rowPtr) and np.array_equal(A.colIndices, C.colIndices)
+    assert np.array_equal(A.values.view(np.uint64), C.values.view(np.uint64))
