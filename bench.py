@@ -73,7 +73,7 @@ def measured_traffic(config: str, kernel: str):
 
 def kernel_label(variant: str, K: int, plan_stats: dict) -> str:
     if variant == "NONZERO":
-        return "k_merge + k_carry_fixup"
+        return "k_merge_flat + k_carry_fixup" if K % 32 == 0 else "k_merge + k_carry_fixup"
     if plan_stats.get("tiled"):
         return "k_rows_pipe<0, 0>" if os.environ.get("SMFV_TILE_KERNEL") == "pipe" else "k_rows_ws"
     if K % 2:
@@ -422,6 +422,10 @@ def main() -> None:
                          "algorithmic_bytes_per_launch": prob_bytes,
                          "avg_launch_ms": round(kern_ms, 6),
                          "timing": "HIP events around one hipGraph replay of all timed launches"},
+            "gather_model": ({"bytes_per_launch": prob_bytes + 8 * nnz * K,
+                              "GBps": round((prob_bytes + 8 * nnz * K) / (kern_ms * 1e-3) / 1e9, 1),
+                              "note": "random columns: one X row gathered per non-zero (SURVEY 8d config 4)"}
+                             if kind == "pow10m" else None),
             "warm": {"note": "same copy every launch (working set in the 256 MiB Infinity Cache)",
                      "avg_launch_ms": round(kern_ms_w, 6), "achieved_GBps": round(achieved_w, 1),
                      "GFLOPs": round(world * flops / (span_ms_w / args.steps * 1e-3) / 1e9, 3)},

@@ -1048,6 +1048,102 @@ __global__ __launch_bounds__(256) void k_merge(int row_first, int nrows, int64_t
     if (tl == 0) carry_row[t] = carried ? i1 : -1;
 }
 
+// k_merge_flat: k_merge for 16-byte columns and K % 32 == 0 with the team's
+// non-zeros streamed flat, across row boundaries: 16 (col, val) pairs per
+// coalesced load (one per lane, broadcast by shuffle), all 16 X-row gathers
+// in flight, then summed in order; a row end met on the way stores the row
+// (row ends of the next 16 rows are held one per lane).  Short rows (most of
+// a power-law matrix) no longer cap the gathers in flight at their length.
+// Same split, carries and per-row summation order as k_merge.
+template <int TEAM>
+__global__ __launch_bounds__(256) void k_merge_flat(int row_first, int nrows, int64_t s, int64_t e,
+                                                    const int *__restrict__ rp, const int *__restrict__ ci,
+                                                    const double *__restrict__ va,
+                                                    const double *__restrict__ X, int64_t ldx, int K,
+                                                    double *__restrict__ Yc, int64_t ldy, int64_t ipt,
+                                                    int64_t nteams, int *__restrict__ carry_row,
+                                                    double *__restrict__ carry_val)
+{
+    static_assert(TEAM == 16, "one 256-B X row per team gather (K panel of 32 doubles)");
+    constexpr int TPB = 256 / TEAM, U = TEAM;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int64_t t = (int64_t)blk * TPB + (threadIdx.x / TEAM);
+    if (t >= nteams) return;
+    const int lane = threadIdx.x & 63;
+    const int tl = lane & (TEAM - 1), tbase = lane & ~(TEAM - 1);
+    const int64_t total = (int64_t)nrows + (e - s);
+    const int64_t d0 = t * ipt;
+    const int64_t d1 = d0 + ipt < total ? d0 + ipt : total;
+    const int i0 = merge_search(rp, row_first, nrows, s, e, d0);
+    const int i1 = merge_search(rp, row_first, nrows, s, e, d1);
+    const int64_t j0 = d0 - i0, j1 = d1 - i1;  // relative nnz positions
+    // the row open at the range end is carried if this team holds >= 1 of its non-zeros
+    bool carried = false;
+    if (i1 < nrows) {
+        const int64_t rs0 = rp[row_first + i1];
+        const int64_t rs = (rs0 > s ? rs0 : s) - s;
+        carried = j1 > (rs > j0 ? rs : j0);
+    }
+    for (int p = 0; p < K / 32; ++p) {
+        const int c = p * 32 + 2 * tl;
+        double2 acc = make_double2(0.0, 0.0);
+        int i = i0;
+        int wbase = i0;  // lane l holds the end of row wbase + l
+        int64_t myend = wbase + tl < nrows ? merge_row_end(rp, row_first, wbase + tl, s, e) : INT64_MAX;
+        auto row_end = [&](int r) -> int64_t {
+            if (r - wbase >= TEAM) {  // team-uniform: slide the window
+                wbase = r;
+                myend = wbase + tl < nrows ? merge_row_end(rp, row_first, wbase + tl, s, e) : INT64_MAX;
+            }
+            return __shfl(myend, tbase + (r - wbase));
+        };
+        int64_t rend = i < i1 ? row_end(i) : INT64_MAX;
+        auto flush_until = [&](int64_t j) {  // store every row (< i1) that ends at or before j
+            while (i < i1 && rend <= j) {
+                *reinterpret_cast<double2 *>(Yc + (int64_t)i * ldy + c) = acc;
+                acc = make_double2(0.0, 0.0);
+                ++i;
+                rend = i < i1 ? row_end(i) : INT64_MAX;
+            }
+        };
+        // (col, val) of the next chunk are loaded while this chunk's gathers fly
+        int nc = 0;
+        double nv = 0.0;
+        if (j0 + tl < j1) {
+            nc = ci[s + j0 + tl];
+            nv = va[s + j0 + tl];
+        }
+        for (int64_t jb = j0; jb < j1; jb += U) {
+            const int n = (int)(j1 - jb < U ? j1 - jb : U);
+            const int myc = nc;
+            const double myv = nv;
+            double2 x[U];
+            double vv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int cc = __shfl(myc, tbase + u);
+                vv[u] = __shfl(myv, tbase + u);
+                x[u] = make_double2(0.0, 0.0);
+                if (u < n) x[u] = *reinterpret_cast<const double2 *>(X + (int64_t)cc * ldx + c);
+            }
+            if (jb + U + tl < j1) {
+                nc = ci[s + jb + U + tl];
+                nv = va[s + jb + U + tl];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (u < n) {
+                    flush_until(jb + u);
+                    acc = VecT<2>::madd(acc, vv[u], x[u]);
+                }
+            }
+        }
+        flush_until(INT64_MAX - 1);  // rows ending at j1 (and empty rows before i1)
+        if (carried) *reinterpret_cast<double2 *>(carry_val + t * K + c) = acc;
+    }
+    if (tl == 0) carry_row[t] = carried ? i1 : -1;
+}
+
 // one thread per (team, column): the first team of each run of equal carry
 // rows sums the run in team order and adds it to the stored row.
 __global__ __launch_bounds__(256) void k_carry_fixup(int64_t nteams, int K,
@@ -1288,7 +1384,7 @@ MergeGeom merge_geom(int nrows, int64_t nnz, int K)
     MergeGeom g;
     g.items = (int64_t)nrows + nnz;
     // ~64 teams per CU on 256 CUs, at least 32 items per team
-    const int64_t target = 256 * 64;
+    const int64_t target = 256 * 64;  // (32-256 per CU measured equal on config 4)
     g.ipt = (g.items + target - 1) / target;
     if (g.ipt < 32) g.ipt = 32;
     (void)K;
@@ -1324,11 +1420,21 @@ static int launch_merge(int row_first, int nrows, int64_t s, int64_t e, const in
     const int tpb = 256 / team;
     const int64_t nblk = (g.nteams + tpb - 1) / tpb;
     SMFV_REQUIRE(nblk <= 0x7fffffff, "too many merge teams for one launch");
+    static const bool flat = [] {  // A/B: SMFV_MERGE_FLAT=0 keeps the per-row k_merge
+        const char *ev = std::getenv("SMFV_MERGE_FLAT");
+        return !ev || std::atoi(ev) != 0;
+    }();
+    if (flat && vec == 2 && K % 32 == 0) {
+        const int64_t fblk_ = (g.nteams + 15) / 16;
+        hipLaunchKernelGGL((k_merge_flat<16>), dim3((unsigned)fblk_), dim3(256), 0, st, row_first, nrows, s, e, rp,
+                           ci, va, X, ldx, K, Yc, ldy, g.ipt, g.nteams, carry_row, carry_val);
+    } else {
 #define L(T_, V_) hipLaunchKernelGGL((k_merge<T_, V_>), dim3((unsigned)nblk), dim3(256), 0, st, \
                                      row_first, nrows, s, e, rp, ci, va, X, ldx, K, Yc, ldy,    \
                                      g.ipt, g.nteams, carry_row, carry_val)
-    SMFV_TEAM_SWITCH(team, vec, L)
+        SMFV_TEAM_SWITCH(team, vec, L)
 #undef L
+    }
     SMFV_LAUNCHED();
     const int64_t nthr = g.nteams * (int64_t)K;
     const int64_t fblk = (nthr + 255) / 256;
