@@ -292,7 +292,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         for (int s = 0; s < WS_ROWS; ++s) lrec[s] = -1;
         int64_t e = 0;
         for (int q = 0; 4 * q < (int)R.size(); ++q) {
-            const int w = q % 8, h = q / 8;
+            const int o = q / 2, w = o < 4 ? o : 11 - o, h = q % 2;  // octet o -> wave; SIMD s runs octets s and 7 - s
             const int nb = len8(R[4 * q]) / 8;
             const int lbase = (int)(e / 8), vbase = (int)(e / 2);
             P.loff.resize((size_t)(noff + e + 32 * nb), (uint16_t)WS_ZOFF);

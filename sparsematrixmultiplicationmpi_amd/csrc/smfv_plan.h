@@ -82,7 +82,9 @@ std::vector<int> pack_tile_records(const TileAnalysis &A);
 // the cop20k_A surrogate number <= 8 per CU (1,980 tiles: every block runs
 // 8, where 2,081 tiles of the former 255 / 1,536 caps made some run 9).
 // Rows are sorted by decreasing length and dealt in quads (4 teams of one
-// lane group, similar lengths); a quad's entries are interleaved in 16-byte
+// lane group, similar lengths), two quads (8 consecutive rows) per compute
+// wave, and the waves sharing a SIMD (w, w + 4) take a long and a short
+// octet; a quad's entries are interleaved in 16-byte
 // chunks (batch b of team k at chunk base + 4b + k, value pair c at chunk
 // base + 4c + k) so one meta read of a lane group touches four bank groups.
 // ---------------------------------------------------------------------------
