@@ -149,6 +149,31 @@ def cpu_baseline(A, K: int, variant: str, budget_s: float = 20.0) -> dict:
             "seconds_per_call": t}
 
 
+def stream_copy_gbps(dev, nbytes: int = 2 << 30, reps: int = 5) -> float:
+    """Measured HBM copy rate on this GPU (read + write bytes / time of a
+    2 GiB copy by the library's 16-byte non-temporal copy kernel,
+    smfv_stream_copy): the practical ceiling next to the 8 TB/s spec that
+    roofline.peak quotes ('measure a STREAM-copy peak')."""
+    import torch
+    from sparsematrixmultiplicationmpi_amd._lib import call
+    a = torch.empty(nbytes // 8, dtype=torch.float64, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    st = torch.cuda.current_stream().cuda_stream
+    call("smfv_stream_copy", b.data_ptr(), a.data_ptr(), nbytes, st)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        call("smfv_stream_copy", b.data_ptr(), a.data_ptr(), nbytes, st)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    torch.cuda.empty_cache()
+    return 2.0 * nbytes / (ms * 1e-3) / 1e9
+
+
 def vendor_leg(copies, args, timed, flops: float):
     """rocSPARSE generic SpMM (the PETSc-block analogue, SC/main.cpp:289-402)
     on the same resident copies, same rotation and graph timing as the
@@ -379,6 +404,7 @@ def main() -> None:
 
     span_ms = timed(capture(False))
     span_ms_w = timed(capture(True))
+    stream_gbps = stream_copy_gbps(dev)
     vendor = None
     if variant in ("ROWWISE", "SEQUENTIAL") and not args.no_vendor:
         vendor = vendor_leg(copies, args, timed, 2.0 * nnz * K)
@@ -421,7 +447,9 @@ def main() -> None:
                          "kernel": kname,
                          "algorithmic_bytes_per_launch": prob_bytes,
                          "avg_launch_ms": round(kern_ms, 6),
-                         "timing": "HIP events around one hipGraph replay of all timed launches"},
+                         "timing": "HIP events around one hipGraph replay of all timed launches",
+                         "stream_copy_GBps": round(stream_gbps, 1),
+                         "frac_of_stream_copy": round(achieved / stream_gbps, 4) if stream_gbps else None},
             "gather_model": ({"bytes_per_launch": prob_bytes + 8 * nnz * K,
                               "GBps": round((prob_bytes + 8 * nnz * K) / (kern_ms * 1e-3) / 1e9, 1),
                               "note": "random columns: one X row gathered per non-zero (SURVEY 8d config 4)"}

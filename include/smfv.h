@@ -132,6 +132,12 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
 SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[6]);
 SMFV_API int smfv_plan_destroy(smfv_plan_t plan);
 
+/* HBM streaming probe for the bench (not the SpMM path): d_dst = d_src,
+ * `bytes` (multiple of 16, 16-B aligned pointers) by a 16-byte-per-lane
+ * non-temporal copy kernel.  Read + write bytes / time = the measured
+ * streaming ceiling quoted beside the 8 TB/s spec. */
+SMFV_API int smfv_stream_copy(void *d_dst, const void *d_src, size_t bytes, void *stream);
+
 /* Rank-local building blocks of the distributed variants (also usable on
  * their own).  Row block [row_begin, row_end) of Y (row-major, ldy):
  * what one rank of SC/...RowWise.cpp:36-50 computes.  n = rows of X (all

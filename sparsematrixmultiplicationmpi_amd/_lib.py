@@ -84,6 +84,7 @@ _SIGS = {
                                    c_void_p, c_size_t, c_void_p]),
     "smfv_dist_rowpart_spmm_f64": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                            c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "smfv_stream_copy": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "smfv_vendor_spmm_create": (c_int, [c_void_p, c_int, c_int, c_int, c_int64, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64, c_void_p]),
     "smfv_vendor_spmm_execute": (c_int, [c_void_p]),

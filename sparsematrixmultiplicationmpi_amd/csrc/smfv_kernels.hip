@@ -961,6 +961,23 @@ __global__ __launch_bounds__(256) void k_rows_list(int nrows, const int *__restr
     *reinterpret_cast<double2 *>(y + 16 * (par ^ 1)) = acc1;
 }
 
+// HBM streaming probe (bench only): 16-byte vector copy, one 16-KiB chunk
+// per 256-lane block (4 loads in flight per lane), non-temporal both ways
+// (6.2 TB/s on the box, against 5.8 with plain loads): the "measured
+// STREAM-copy peak" next to the 8 TB/s spec.
+__global__ __launch_bounds__(256) void k_copy16(int64_t n16, const ws::d2 *__restrict__ src,
+                                                ws::d2 *__restrict__ dst)
+{
+    const int64_t base = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+    ws::d2 a[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (base + 256 * k < n16) a[k] = __builtin_nontemporal_load(src + base + 256 * k);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (base + 256 * k < n16) __builtin_nontemporal_store(a[k], dst + base + 256 * k);
+}
+
 // plan value binding: tile-ordered copy of A's values (pads -> pad)
 __global__ __launch_bounds__(256) void k_gather_vals(int64_t count, const int *__restrict__ tsrc,
                                                      const double *__restrict__ va,
@@ -1757,6 +1774,18 @@ SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, voi
         SMFV_LAUNCHED();
     }
     plan->bound_values = d_values;
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_stream_copy(void *d_dst, const void *d_src, size_t bytes, void *stream)
+{
+    SMFV_REQUIRE(d_dst && d_src && aligned16(d_dst) && aligned16(d_src) && bytes % 16 == 0,
+                 "copy needs 16-byte aligned pointers and size");
+    if (bytes == 0) return SMFV_OK;
+    const int64_t n16 = (int64_t)(bytes / 16), nblk = (n16 + 1023) / 1024;
+    SMFV_REQUIRE(nblk <= 0x7fffffff, "copy too large");
+    hipLaunchKernelGGL(k_copy16, dim3((unsigned)nblk), dim3(256), 0, as_stream(stream), n16, static_cast<const ws::d2 *>(d_src), static_cast<ws::d2 *>(d_dst));
+    SMFV_LAUNCHED();
     return SMFV_OK;
 }
 
