@@ -904,6 +904,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
             for (int b = 0; b < nbat; ++b) {
                 rdx(ln.z, xc0[0], xc1[0], xc0[1], xc1[1]);  // second half of batch b
                 rdx(ln.w, xc0[2], xc1[2], xc0[3], xc1[3]);
+                __builtin_amdgcn_sched_barrier(0);
                 const double v[8] = {vn[0].x, vn[0].y, vn[1].x, vn[1].y, vn[2].x, vn[2].y, vn[3].x, vn[3].y};
                 // next batch's meta (the last batch re-reads itself); volatile
                 // keeps these reads here, behind this batch's X reads
@@ -919,6 +920,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
                 }
                 rdx(ln.x, xa0[0], xa1[0], xa0[1], xa1[1]);  // first half of batch b + 1
                 rdx(ln.y, xa0[2], xa1[2], xa0[3], xa1[3]);
+                __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the second half's FP64
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     acc0 = acc0 + v[4 + k] * xc0[k];
