@@ -774,7 +774,10 @@ __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(
 }  // namespace ws
 
 // ABL (lab A/B only, SMFV_WS_ABL): 1 staging only (no compute), 2 compute
-// only (every unit recomputes the first staged tile), 3 as 2 without Y stores
+// only (every unit recomputes the first staged tile), 3 as 2 without Y stores,
+// 4 as 2 without the per-unit barriers (waves run their units unsynchronised),
+// 5 staging and compute both running, decoupled (no barriers; compute reads
+// slot 0 while it is restaged: timing only, results are garbage)
 template <int ABL>
 __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
@@ -853,14 +856,14 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
         int it = 0, p = 0;  // unit u + 1 to stage
         if (++p == npanel) p = 0, ++it;
         for (int u = 0; u < nunits; ++u) {
-            if (u + 1 < nunits && ABL != 2 && ABL != 3) {
+            if (u + 1 < nunits && ABL != 2 && ABL != 3 && ABL != 4) {
                 const int t = t0 + it * tstep;
                 stage(t, p, (u + 1) & 1, it & 1);
                 if (p == npanel - 1) fetch_record(min(t + tstep, tlast));
                 if (++p == npanel) p = 0, ++it;
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // unit u+1 has landed
-            barrier_lds();
+            if (ABL != 4 && ABL != 5) barrier_lds();
         }
         return;
     }
@@ -934,7 +937,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
             }
         }
         if (++p == npanel) p = 0, ++it;
-        barrier_lds();  // X slot (u & 1) is free for unit u + 2, meta slot for tile it + 1
+        if (ABL != 4 && ABL != 5) barrier_lds();  // X slot (u & 1) is free for unit u + 2, meta slot for tile it + 1
     }
 }
 
@@ -1841,7 +1844,8 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
                     const char *e = std::getenv("SMFV_WS_ABL");
                     return e ? std::atoi(e) : 0;
                 }();
-                hipLaunchKernelGGL(abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3> : k_rows_ws<0>, dim3((unsigned)blocks), dim3(1024), 0, as_stream(stream), plan->ntiles,
+                hipLaunchKernelGGL(abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3>
+                                   : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : k_rows_ws<0>, dim3((unsigned)blocks), dim3(1024), 0, as_stream(stream), plan->ntiles,
                                    K / TILE_KP, plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx,
                                    d_Y, ldy);
                 SMFV_LAUNCHED();
