@@ -75,7 +75,7 @@ def kernel_label(variant: str, K: int, plan_stats: dict) -> str:
     if variant == "NONZERO":
         return "k_merge_flat + k_carry_fixup" if K % 32 == 0 else "k_merge + k_carry_fixup"
     if plan_stats.get("tiled"):
-        return "k_rows_pipe<0, 0>" if os.environ.get("SMFV_TILE_KERNEL") == "pipe" else "k_rows_ws"
+        return "k_rows_ws"
     if K % 2:
         return "k_rows<TEAM,1>"
     pairs = K // 2

@@ -2,16 +2,19 @@
 // hot path and the single-device C ABI (include/smfv.h).
 //
 // Reference loops replaced (SC = /root/reference/Source Code):
-//   k_rows   <- SC/SparseMatrixFatVectorMultiply.cpp:17-27 (sequential) and
+//   k_rows_ws (tiled plan, K % 32 == 0), k_rows_mh / k_rows (no plan),
+//   k_rows_list (a plan's direct rows)
+//            <- SC/SparseMatrixFatVectorMultiply.cpp:17-27 (sequential) and
 //               SC/SparseMatrixFatVectorMultiplyRowWise.cpp:36-50 (row block)
-//   k_rows with a column window (colpanel)
+//   the same with a column window (colpanel)
 //            <- SC/SparseMatrixFatVectorMultiplyColumnWise.cpp:34-48
-//   k_merge + k_carry_fixup
+//   k_merge_flat / k_merge + k_carry_fixup
 //            <- SC/SparseMatrixFatVectorMultiplyNonZeroElement.cpp:24-67 (nnz
 //               partition) + :88 (sum of partial rows)
 //   k_panels_to_rowmajor <- SC/...ColumnWise.cpp:109-126 (rank-0 rebuild)
 //   k_combine_blocks     <- SC/...NonZeroElement.cpp:88 (MPI_Reduce SUM)
 //   k_compare            <- SC/utils.cpp:38-63 (areMatricesEqual)
+//   k_copy16             bench probe: measured HBM streaming rate
 //
 // Layout: X[n x K] and Y[m x K] row-major (SC/utils.cpp:216-228 serialize),
 // CSR int32/f64 as SC/MatrixDefinitions.h:14-19.
@@ -321,402 +324,6 @@ __global__ __launch_bounds__(256) void k_rows_mh(int row_begin, int nrows,
             for (int h = 0; h < H; ++h)
                 if (ok[h]) *reinterpret_cast<double2 *>(yrow + cb + 2 * TEAM * h) = acc[h];
     }
-}
-
-// ---------------------------------------------------------------------------
-// k_rows_tiled: one workgroup per row tile (<= 32 rows clustered by the plan,
-// smfv_plan.cpp) and per 32-column panel of X / Y.
-//   0. the tile record (TileMeta, 32 B) is one scalar load;
-//   1. each lane loads the union ids of the X rows it will copy, plus (per
-//      team) its row id and tile-local non-zero range;
-//   2. LDS-DMA (global_load_lds_dwordx4): the tile's distinct X rows (the
-//      panel's 256-B slice each, 4 rows per wave-instruction) into a dense
-//      [u][32] image, and the tile's non-zeros -- tile-ordered copies of the
-//      values (f64) and 16-bit union positions owned by the plan -- into LDS;
-//   3. an 8-lane team per row (8 rows per wave) walks the row's non-zeros in
-//      CSR order; lane t of team T holds columns {2t, 2t+1} of both 128-B
-//      halves of the X row and reads half (h ^ (T & 1)) in its h-th
-//      ds_read_b128, which keeps the 8 rows a wave reads bank-conflict-free.
-// Each staged X row serves ~4 non-zeros on mesh-like patterns, so the
-// CU-side row-gather traffic (the bound of the untiled kernel) drops by that
-// factor.  A "direct" tile (one row over a cap) gathers X straight from HBM.
-// Per-row order and arithmetic are the reference's.
-// ---------------------------------------------------------------------------
-template <int MODE>  // 0 = production; lab ablations: 1 = stage only, 2 = compute only
-__global__ __launch_bounds__(256) void k_rows_tiled(
-    const TileMeta *__restrict__ meta, const int *__restrict__ trows, const int *__restrict__ rbeg,
-    const int *__restrict__ ucols, const uint16_t *__restrict__ tlidx,
-    const double *__restrict__ tvals, const int *__restrict__ rp, const int *__restrict__ ci,
-    const double *__restrict__ va, const double *__restrict__ X, int64_t ldx, int K,
-    double *__restrict__ Y, int64_t ldy)
-{
-    __shared__ __attribute__((aligned(16))) double s_x[TILE_UCAP * TILE_KP];
-    __shared__ __attribute__((aligned(16))) double s_va[TILE_NCAP];
-    __shared__ __attribute__((aligned(16))) uint16_t s_li[TILE_NCAP];
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
-    const int cp = blockIdx.y * TILE_KP;  // first column of this panel
-    const TileMeta tm = meta[t];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int team = tid >> 3, tl = tid & 7, par = team & 1;
-    const bool live = team < tm.nrows;
-    int row = 0, js = 0, je = 0;
-    if (live) {
-        row = trows[tm.roff + team];
-        const int info = rbeg[tm.roff + team];  // start (multiple of 8) | len << 16
-        js = info & 0xFFFF;
-        je = js + (info >> 16);
-    }
-    double2 acc0 = make_double2(0.0, 0.0), acc1 = make_double2(0.0, 0.0);
-    if (!tm.direct) {
-        // X rows: wave w copies groups g = w, w+4, ... of 4 union rows
-        constexpr int GPW = TILE_UCAP / 16;  // groups per wave
-        if constexpr (MODE != 2) {
-        int src_row[GPW];
-#pragma unroll
-        for (int k = 0; k < GPW; ++k) {
-            const int u = min((wave + 4 * k) * 4 + (lane >> 4), max(tm.nu - 1, 0));
-            src_row[k] = tm.nu > 0 ? ucols[tm.uoff + u] : 0;
-        }
-#pragma unroll
-        for (int k = 0; k < GPW; ++k) {
-            const int g = wave + 4 * k;
-            if (g * 4 < tm.nu) {
-                const double *src = X + (int64_t)src_row[k] * ldx + cp + 2 * (lane & 15);
-                __builtin_amdgcn_global_load_lds((const void *)src,
-                                                 (__attribute__((address_space(3))) void *)(s_x + g * 128),
-                                                 16, 0, 0);
-            }
-        }
-        // values: 128 doubles per wave-instruction; local columns: 512 u16
-        const int tn8 = (tm.tn + 7) & ~7;  // padded segment (multiple of 8)
-        for (int v = wave; v * 128 < tn8; v += 4) {
-            const int e = min(v * 128 + 2 * lane, tn8 - 2);
-            __builtin_amdgcn_global_load_lds((const void *)(tvals + tm.noff + e),
-                                             (__attribute__((address_space(3))) void *)(s_va + v * 128),
-                                             16, 0, 0);
-        }
-        for (int v = wave; v * 512 < tn8; v += 4) {
-            const int e = min(v * 512 + 8 * lane, tn8 - 8);
-            __builtin_amdgcn_global_load_lds((const void *)(tlidx + tm.noff + e),
-                                             (__attribute__((address_space(3))) void *)(s_li + v * 512),
-                                             16, 0, 0);
-        }
-        }  // MODE != 2
-        __syncthreads();  // drains the LDS-DMA (vmcnt(0)) and publishes the tile
-        if (!live) return;
-        constexpr int U = 8;
-        if constexpr (MODE == 1) je = js;  // lab: stage only
-        const double2 *sx0 = reinterpret_cast<const double2 *>(s_x) + par * 8 + tl;
-        const double2 *sx1 = reinterpret_cast<const double2 *>(s_x) + (par ^ 1) * 8 + tl;
-        int j = js;
-        for (; j + U <= je; j += U) {
-            double2 x0[U], x1[U];
-            double v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int l = s_li[j + u];
-                v[u] = s_va[j + u];
-                x0[u] = sx0[l * (TILE_KP / 2)];
-                x1[u] = sx1[l * (TILE_KP / 2)];
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                acc0 = VecT<2>::madd(acc0, v[u], x0[u]);
-                acc1 = VecT<2>::madd(acc1, v[u], x1[u]);
-            }
-        }
-        for (; j < je; ++j) {
-            const int l = s_li[j];
-            const double v = s_va[j];
-            acc0 = VecT<2>::madd(acc0, v, sx0[l * (TILE_KP / 2)]);
-            acc1 = VecT<2>::madd(acc1, v, sx1[l * (TILE_KP / 2)]);
-        }
-    } else {
-        if (!live) return;
-        // one wide row: gather X directly, same lane -> column mapping
-        for (int jj = rp[row]; jj < rp[row + 1]; ++jj) {
-            const double *px = X + (int64_t)ci[jj] * ldx + cp + 2 * tl;
-            const double v = va[jj];
-            acc0 = VecT<2>::madd(acc0, v, *reinterpret_cast<const double2 *>(px + 16 * par));
-            acc1 = VecT<2>::madd(acc1, v, *reinterpret_cast<const double2 *>(px + 16 * (par ^ 1)));
-        }
-    }
-    double *y = Y + (int64_t)row * ldy + cp + 2 * tl;
-    *reinterpret_cast<double2 *>(y + 16 * par) = acc0;
-    *reinterpret_cast<double2 *>(y + 16 * (par ^ 1)) = acc1;
-}
-
-// ---------------------------------------------------------------------------
-// k_rows_pipe: the production tiled kernel.  Persistent blocks (a few per
-// CU), each walking a contiguous range of tiles; tile t+1 is prefetched into
-// registers (X rows, values, local columns, and the record of tile t+2)
-// while tile t is computed from LDS, then written to LDS after a barrier
-// (register staging: ordinary loads only, so hipcc's own wait counts stay
-// exact).  Per tile the dependent global round trips (record -> union ids ->
-// X rows) are hidden behind the previous tile's compute.  LDS per block:
-// X image 32 KiB + values 8 KiB + local columns 2 KiB + 2 records 2 KiB.
-// Compute is k_rows_tiled's: 8-lane teams, conflict-free swizzled halves,
-// CSR order, separate multiply / add.
-// ---------------------------------------------------------------------------
-typedef double pipe_d2 __attribute__((ext_vector_type(2)));
-typedef unsigned pipe_u2 __attribute__((ext_vector_type(2)));
-// Registers of the tile in flight (native vector types: HIP's union-based
-// double2 in a conditionally written aggregate is demoted to scratch).
-struct PipeStage {
-    pipe_d2 x[TILE_UCAP / 16];  // 8 x 16 B of union rows (tid>>4) + 16k
-    pipe_d2 v[2];               // 4 values
-    pipe_u2 l;                  // 4 local columns (u16)
-    int rec;                    // one word of the record two tiles ahead
-};
-
-__device__ __forceinline__ void pipe_load(PipeStage &S, const int *R, const uint16_t *__restrict__ tlidx,
-                                          const double *__restrict__ tvals,
-                                          const double *__restrict__ X, int64_t ldx, int cp, int tid)
-{
-    const int noff = R[0], tn = R[1], nu = R[3], direct = R[6];
-    if (direct) return;
-    const int xr = tid >> 4, xs = tid & 15;
-    // the record stores union id u at TREC_UCOLS + (u % 16) * 8 + u / 16, so
-    // this thread's 8 ids (u = xr + 16k) are two aligned 16-byte LDS reads
-    const int4 c0 = *reinterpret_cast<const int4 *>(R + TREC_UCOLS + 8 * xr);
-    const int4 c1 = *reinterpret_cast<const int4 *>(R + TREC_UCOLS + 8 * xr + 4);
-    const int uc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-#pragma unroll
-    for (int k = 0; k < TILE_UCAP / 16; ++k) {
-        const int u = xr + 16 * k;
-        if (u < nu)
-            S.x[k] = *reinterpret_cast<const pipe_d2 *>(X + (int64_t)uc[k] * ldx + cp + 2 * xs);
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int e = 2 * tid + 512 * k;
-        if (e < tn) S.v[k] = *reinterpret_cast<const pipe_d2 *>(tvals + noff + e);
-    }
-    if (4 * tid < tn) S.l = *reinterpret_cast<const pipe_u2 *>(tlidx + noff + 4 * tid);
-}
-
-__device__ __forceinline__ void pipe_store(const PipeStage &S, const int *R, double *s_x, double *s_va,
-                                           uint16_t *s_li, int tid)
-{
-    const int tn = R[1], nu = R[3], direct = R[6];
-    if (direct) return;
-    const int xr = tid >> 4, xs = tid & 15;
-#pragma unroll
-    for (int k = 0; k < TILE_UCAP / 16; ++k) {
-        const int u = xr + 16 * k;
-        if (u < nu) reinterpret_cast<pipe_d2 *>(s_x)[u * (TILE_KP / 2) + xs] = S.x[k];
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int e = 2 * tid + 512 * k;
-        if (e < tn) reinterpret_cast<pipe_d2 *>(s_va)[e / 2] = S.v[k];
-    }
-    if (4 * tid < tn) reinterpret_cast<pipe_u2 *>(s_li)[tid] = S.l;
-}
-
-// B8: 0 = batches of 4 + single tail steps, 1 = masked batches of 8,
-// 2 = software-pipelined masked batches of 4.
-// ABL (lab only): 0 production, 1 no compute, 2 no prefetch of X / CSR, 3 neither,
-// 4 production with per-wave phase timestamps into prof (scripts/micro).
-template <int B8, int ABL>
-__global__ __launch_bounds__(256, 3) void k_rows_pipe(  // 3 waves / SIMD = the LDS limit
-    int ntiles, const int *__restrict__ rec, const uint16_t *__restrict__ tlidx,
-    const double *__restrict__ tvals, const int *__restrict__ rp, const int *__restrict__ ci,
-    const double *__restrict__ va, const double *__restrict__ X, int64_t ldx, int K,
-    double *__restrict__ Y, int64_t ldy, int interleave, long long *__restrict__ prof)
-{
-    __shared__ __attribute__((aligned(16))) double s_x[TILE_UCAP * TILE_KP];
-    __shared__ __attribute__((aligned(16))) double s_va[TILE_NCAP];
-    __shared__ __attribute__((aligned(16))) uint16_t s_li[TILE_NCAP];
-    __shared__ __attribute__((aligned(16))) int s_rec[2][TREC_WORDS];
-    // Tile order.  interleave (default): XCD x = blockIdx.x % 8 owns the
-    // tiles [ntiles*x/8, ntiles*(x+1)/8); its j-th block takes tiles
-    // first + j, first + j + nb, ... so the XCD's blocks sweep its range
-    // together and consecutive (neighbouring) tiles re-use each other's X
-    // rows from the XCD's L2.  Otherwise each block takes a contiguous run.
-    int t0, tstep, tlast;
-    {
-        const int G = gridDim.x;
-        if (interleave) {
-            const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
-            const int nb = (G >> 3) + (x < (G & 7) ? 1 : 0);
-            const int first = (int)((int64_t)ntiles * x / 8), end = (int)((int64_t)ntiles * (x + 1) / 8);
-            t0 = first + j;
-            tstep = nb;
-            if (t0 >= end) return;  // block-uniform
-            tlast = t0 + ((end - 1 - t0) / nb) * nb;
-        } else {
-            const int b = xcd_remap(blockIdx.x, G);
-            t0 = (int)((int64_t)ntiles * b / G);
-            const int t1 = (int)((int64_t)ntiles * (b + 1) / G);
-            if (t0 >= t1) return;  // block-uniform
-            tstep = 1;
-            tlast = t1 - 1;
-        }
-    }
-    const int cp = blockIdx.y * TILE_KP;
-    const int tid = threadIdx.x, team = tid >> 3, tl = tid & 7, par = team & 1;
-    const long long wall_start = ABL == 4 ? wall_clock64() : 0;
-    PipeStage S;
-    // prologue: record(t0) -> LDS; tile t0 + record(t0 + 1) -> registers -> LDS.
-    // Prefetch indices are clamped to the block's last tile (re-staging it on
-    // the final iteration) so every load is unconditional: a load-or-constant
-    // register would make hipcc drain vmcnt on the loop back-edge.
-    s_rec[0][tid] = rec[(int64_t)t0 * TREC_WORDS + tid];
-    __syncthreads();
-    if (ABL != 2 && ABL != 3) pipe_load(S, s_rec[0], tlidx, tvals, X, ldx, cp, tid);
-    S.rec = rec[(int64_t)min(t0 + tstep, tlast) * TREC_WORDS + tid];
-    if (ABL != 2 && ABL != 3) pipe_store(S, s_rec[0], s_x, s_va, s_li, tid);
-    s_rec[1][tid] = S.rec;
-    __syncthreads();
-    const double2 *sx0 = reinterpret_cast<const double2 *>(s_x) + par * 8 + tl;
-    const double2 *sx1 = reinterpret_cast<const double2 *>(s_x) + (par ^ 1) * 8 + tl;
-    long long *pw = nullptr;  // lab: [block][step<15][wave][4]; step 15: wall start / end
-    if constexpr (ABL == 4) {
-        pw = prof + ((int64_t)blockIdx.x * 16 * 4 + (tid >> 6)) * 4;
-        if ((tid & 63) == 0) pw[15 * 16 + 0] = wall_start;
-    }
-    for (int t = t0, it = 0; t <= tlast; t += tstep, ++it) {
-        const int cur = it & 1;
-        if constexpr (ABL == 4)
-            if ((tid & 63) == 0 && it < 15) pw[it * 16 + 0] = clock64();
-        const int *R = s_rec[cur];
-        const int *Rn = s_rec[cur ^ 1];  // record of the next tile (or t itself, last)
-        // prefetch the next tile and the record of the one after it
-        if (ABL != 2 && ABL != 3) pipe_load(S, Rn, tlidx, tvals, X, ldx, cp, tid);
-        S.rec = rec[(int64_t)min(t + 2 * tstep, tlast) * TREC_WORDS + tid];
-        // compute tile t
-        const int nrows = R[5], direct = R[6];
-        if (team < nrows) {
-            const int row = R[TREC_ROWS + team];
-            double2 acc0 = make_double2(0.0, 0.0), acc1 = make_double2(0.0, 0.0);
-            if (!direct) {
-                const int info = R[TREC_INFO + team];
-                const int js = info & 0xFFFF, je = (ABL == 1 || ABL == 3) ? js : js + (info >> 16);
-                if constexpr (B8 == 2) {
-                    // software-pipelined batches of 4: the X reads of batch i
-                    // go out together with the local columns / values of
-                    // batch i+1 (one LDS round trip per batch); the last batch
-                    // is masked (segments are padded to 8, reads stay inside
-                    // the staged arrays: jn is clamped)
-                    pipe_u2 lq = *reinterpret_cast<const pipe_u2 *>(s_li + js);
-                    pipe_d2 va0 = *reinterpret_cast<const pipe_d2 *>(s_va + js);
-                    pipe_d2 va1 = *reinterpret_cast<const pipe_d2 *>(s_va + js + 2);
-                    for (int j = js; j < je; j += 4) {
-                        const int l[4] = {(int)(lq.x & 0xFFFF), (int)(lq.x >> 16), (int)(lq.y & 0xFFFF),
-                                          (int)(lq.y >> 16)};
-                        double2 x0[4], x1[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            x0[u] = sx0[l[u] * (TILE_KP / 2)];
-                            x1[u] = sx1[l[u] * (TILE_KP / 2)];
-                        }
-                        const double v[4] = {va0.x, va0.y, va1.x, va1.y};
-                        // volatile: keeps these reads here, behind the X reads
-                        // (otherwise they are re-sunk to the next iteration's top)
-                        const int jn = min(j + 4, TILE_NCAP - 4);
-                        lq = *(const volatile __attribute__((address_space(3))) pipe_u2 *)(s_li + jn);
-                        va0 = *(const volatile __attribute__((address_space(3))) pipe_d2 *)(s_va + jn);
-                        va1 = *(const volatile __attribute__((address_space(3))) pipe_d2 *)(s_va + jn + 2);
-                        const int live = je - j;
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {  // branch-free mask: keep or discard the sum
-                            const double2 n0 = VecT<2>::madd(acc0, v[u], x0[u]);
-                            const double2 n1 = VecT<2>::madd(acc1, v[u], x1[u]);
-                            const bool ok = u < live;
-                            acc0.x = ok ? n0.x : acc0.x;
-                            acc0.y = ok ? n0.y : acc0.y;
-                            acc1.x = ok ? n1.x : acc1.x;
-                            acc1.y = ok ? n1.y : acc1.y;
-                        }
-                    }
-                } else if constexpr (B8 == 0) {
-                    constexpr int U = 4;
-                    int j = js;
-                    for (; j + U <= je; j += U) {
-                        double2 x0[U], x1[U];
-                        double v[U];
-#pragma unroll
-                        for (int u = 0; u < U; ++u) {
-                            const int l = s_li[j + u];
-                            v[u] = s_va[j + u];
-                            x0[u] = sx0[l * (TILE_KP / 2)];
-                            x1[u] = sx1[l * (TILE_KP / 2)];
-                        }
-#pragma unroll
-                        for (int u = 0; u < U; ++u) {
-                            acc0 = VecT<2>::madd(acc0, v[u], x0[u]);
-                            acc1 = VecT<2>::madd(acc1, v[u], x1[u]);
-                        }
-                    }
-                    for (; j < je; ++j) {
-                        const int l = s_li[j];
-                        const double v = s_va[j];
-                        acc0 = VecT<2>::madd(acc0, v, sx0[l * (TILE_KP / 2)]);
-                        acc1 = VecT<2>::madd(acc1, v, sx1[l * (TILE_KP / 2)]);
-                    }
-                } else {
-                    // batches of 8: the row segment starts 8-aligned and is
-                    // padded to a multiple of 8, so one b128 read brings 8 local
-                    // columns, four bring 8 values; entries past the row end
-                    // are read but not summed (the sum stays the CSR-order sum)
-                    constexpr int U = 4;
-                    for (int j = js; j < je; j += 8) {
-                        const uint4 lq = *reinterpret_cast<const uint4 *>(s_li + j);
-                        const pipe_d2 *vq = reinterpret_cast<const pipe_d2 *>(s_va + j);
-                        double v[8];
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const pipe_d2 t2 = vq[q];
-                            v[2 * q] = t2.x;
-                            v[2 * q + 1] = t2.y;
-                        }
-                        const unsigned lw[4] = {lq.x, lq.y, lq.z, lq.w};
-                        const int live = je - j;
-#pragma unroll
-                        for (int h = 0; h < 8; h += U) {  // X gathered U at a time
-                            double2 x0[U], x1[U];
-#pragma unroll
-                            for (int u = 0; u < U; ++u) {
-                                const int l = (lw[(h + u) >> 1] >> (16 * ((h + u) & 1))) & 0xFFFF;
-                                x0[u] = sx0[l * (TILE_KP / 2)];
-                                x1[u] = sx1[l * (TILE_KP / 2)];
-                            }
-#pragma unroll
-                            for (int u = 0; u < U; ++u) {
-                                if (h + u < live) {
-                                    acc0 = VecT<2>::madd(acc0, v[h + u], x0[u]);
-                                    acc1 = VecT<2>::madd(acc1, v[h + u], x1[u]);
-                                }
-                            }
-                        }
-                    }
-                }
-            } else {
-                for (int jj = rp[row]; jj < rp[row + 1]; ++jj) {
-                    const double *px = X + (int64_t)ci[jj] * ldx + cp + 2 * tl;
-                    const double v = va[jj];
-                    acc0 = VecT<2>::madd(acc0, v, *reinterpret_cast<const double2 *>(px + 16 * par));
-                    acc1 = VecT<2>::madd(acc1, v, *reinterpret_cast<const double2 *>(px + 16 * (par ^ 1)));
-                }
-            }
-            double *y = Y + (int64_t)row * ldy + cp + 2 * tl;
-            *reinterpret_cast<double2 *>(y + 16 * par) = acc0;
-            *reinterpret_cast<double2 *>(y + 16 * (par ^ 1)) = acc1;
-        }
-        if constexpr (ABL == 4)
-            if ((tid & 63) == 0 && it < 15) pw[it * 16 + 1] = clock64();
-        __syncthreads();  // tile t's LDS image and record are no longer read
-        if constexpr (ABL == 4)
-            if ((tid & 63) == 0 && it < 15) pw[it * 16 + 2] = clock64();
-        if (ABL != 2 && ABL != 3) pipe_store(S, Rn, s_x, s_va, s_li, tid);
-        s_rec[cur][tid] = S.rec;  // record of t+2 takes tile t's slot
-        if constexpr (ABL == 4)
-            if ((tid & 63) == 0 && it < 15) pw[it * 16 + 3] = clock64();
-        __syncthreads();
-    }
-    if constexpr (ABL == 4)
-        if ((tid & 63) == 0) pw[15 * 16 + 1] = wall_clock64();
 }
 
 // ---------------------------------------------------------------------------
@@ -1566,22 +1173,17 @@ struct smfv_plan_s {
     int ntiles = 0, ndirect = 0;
     int64_t union_rows = 0, tiled_nnz = 0, padded_nnz = 0;
     double reuse = 0.0;
-    TileMeta *meta = nullptr;
-    int *trows = nullptr, *rbeg = nullptr, *ucols = nullptr, *tsrc = nullptr, *rec = nullptr;
-    uint16_t *tlidx = nullptr;
-    double *tvals = nullptr;
+    int *tsrc = nullptr;                   // entry -> CSR index of its value (-1: pad)
+    double *tvals = nullptr;               // tile-ordered values (pads -0.0)
     const double *bound_values = nullptr;  // d_values the tile-ordered copy came from
-    // tiled kernel: 0 k_rows_ws (default), 1 k_rows_pipe (SMFV_TILE_KERNEL=pipe, A/B only)
-    int kind = 0;
     int *ws_grec = nullptr, *ws_lrec = nullptr, *direct_rows = nullptr;
     uint16_t *ws_loff = nullptr;
     void *ws = nullptr;
     size_t ws_bytes = 0, dev_bytes = 0;
     ~smfv_plan_s()
     {
-        for (void *q : {(void *)meta, (void *)trows, (void *)rbeg, (void *)ucols, (void *)tsrc,
-                        (void *)rec, (void *)tlidx, (void *)tvals, (void *)ws_grec, (void *)ws_lrec,
-                        (void *)direct_rows, (void *)ws_loff, ws})
+        for (void *q : {(void *)tsrc, (void *)tvals, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
+                        (void *)ws_loff, ws})
             if (q) (void)hipFree(q);
     }
 };
@@ -1625,29 +1227,24 @@ SMFV_API int smfv_plan_create(smfv_plan_t *out, int variant, int m, int n, int64
         }
     } else if (h_row_ptr && h_col_idx && m > 0 && K > 0 && K % TILE_KP == 0 &&
                !(flags & SMFV_PLAN_NO_TILES)) {
-        TileAnalysis T;
         bool go = true;
         if (!(flags & SMFV_PLAN_FORCE_TILES) && m > SMFV_TILE_SAMPLE_ROWS) {
             // estimate re-use on a leading block of rows first (the analysis
             // of the full pattern costs O(nnz * candidates))
             const int ms = SMFV_TILE_SAMPLE_ROWS;
             std::vector<int> rps(h_row_ptr, h_row_ptr + ms + 1);
+            TileAnalysis T;
             analyse_tiles(ms, n, rps.data(), h_col_idx, T);
             const double est = T.union_rows ? (double)T.tiled_nnz / (double)T.union_rows : 0.0;
             go = est >= SMFV_TILE_MIN_REUSE;
         }
-        static const bool use_pipe = [] {
-            const char *e = std::getenv("SMFV_TILE_KERNEL");
-            return e && std::string(e) == "pipe";
-        }();
-        if (go && !use_pipe) {
+        if (go) {
             WsPlan W;
             std::string err;
             if (!build_ws_plan(m, n, h_row_ptr, h_col_idx, W, &err)) {
                 set_error("%s", err.c_str());
                 rc = SMFV_ERR_INVALID;
             } else {
-                p->kind = 0;
                 p->ntiles = W.ntiles;
                 p->union_rows = W.union_rows;
                 p->tiled_nnz = W.tiled_nnz;
@@ -1672,34 +1269,6 @@ SMFV_API int smfv_plan_create(smfv_plan_t *out, int variant, int m, int n, int64
                     }
                 }
             }
-        } else if (go) {
-            p->kind = 1;
-            analyse_tiles(m, n, h_row_ptr, h_col_idx, T);
-            p->ntiles = (int)T.meta.size();
-            p->union_rows = T.union_rows;
-            p->tiled_nnz = T.tiled_nnz;
-            p->padded_nnz = T.padded_nnz;
-            for (const TileMeta &tm : T.meta) p->ndirect += tm.direct;
-            p->reuse = T.union_rows ? (double)T.tiled_nnz / (double)T.union_rows : 0.0;
-            if (p->reuse >= SMFV_TILE_MIN_REUSE || (flags & SMFV_PLAN_FORCE_TILES)) {
-                p->tiled = true;
-                if (!rc) rc = upload(&p->meta, T.meta, p->dev_bytes);
-                if (!rc) rc = upload(&p->trows, T.trows, p->dev_bytes);
-                if (!rc) rc = upload(&p->rbeg, T.rbeg, p->dev_bytes);
-                if (!rc) rc = upload(&p->ucols, T.ucols, p->dev_bytes);
-                if (!rc) rc = upload(&p->tsrc, T.tsrc, p->dev_bytes);
-                if (!rc) rc = upload(&p->rec, pack_tile_records(T), p->dev_bytes);
-                if (!rc) rc = upload(&p->tlidx, T.tlidx, p->dev_bytes);
-                if (!rc) {
-                    const size_t b = std::max<size_t>((size_t)T.padded_nnz, 1) * sizeof(double);
-                    hipError_t e = hipMalloc(reinterpret_cast<void **>(&p->tvals), b);
-                    if (e != hipSuccess) {
-                        set_error("hipMalloc(tvals): %s", hipGetErrorString(e));
-                        rc = SMFV_ERR_HIP;
-                    }
-                    p->dev_bytes += b;
-                }
-            }
         }
     }
     if (rc) {
@@ -1715,19 +1284,20 @@ SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_
 {
     SMFV_REQUIRE(m >= 0 && n >= 0 && h_row_ptr && (h_row_ptr[m] == 0 || h_col_idx) && out,
                  "bad argument");
+    const TileCaps caps;
     TileAnalysis T;
-    analyse_tiles(m, n, h_row_ptr, h_col_idx, T);
-    // invariants the tiled kernel relies on
+    analyse_tiles(m, n, h_row_ptr, h_col_idx, T, caps);
+    // invariants of the clustered analysis the plan is built from
     std::vector<char> seen((size_t)std::max(m, 1), 0);
     int64_t nd = 0;
     for (const TileMeta &tm : T.meta) {
-        SMFV_REQUIRE(tm.nrows >= 1 && tm.nrows <= TILE_MAXROWS, "tile rows out of range");
+        SMFV_REQUIRE(tm.nrows >= 1 && tm.nrows <= caps.maxrows, "tile rows out of range");
         SMFV_REQUIRE(tm.noff % 8 == 0, "tile segment not 16-byte aligned");
         if (tm.direct) {
             ++nd;
             SMFV_REQUIRE(tm.nrows == 1, "direct tile with several rows");
         } else {
-            SMFV_REQUIRE(tm.nu <= TILE_UCAP && tm.tn <= TILE_NCAP, "tile over a cap");
+            SMFV_REQUIRE(tm.nu <= caps.ucap && tm.tn <= caps.ncap, "tile over a cap");
         }
         int local = 0;
         for (int k = 0; k < tm.nrows; ++k) {
@@ -1820,72 +1390,40 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     const int m = plan->m, K = plan->K;
     SMFV_REQUIRE(ldx >= K && ldy >= K, "leading dimension smaller than K");
     if (m == 0 || K == 0) return SMFV_OK;
-    if (plan->tiled && pick_vec(d_X, ldx, d_Y, ldy, K) == 2) {
-        SMFV_REQUIRE(d_row_ptr && d_X && d_Y && d_values, "null argument");
-        if (d_values != plan->bound_values) {
-            set_error("tiled plan: values not bound (call smfv_plan_bind_values with these d_values)");
-            return SMFV_ERR_INVALID;
-        }
-        static const int ablate = [] {  // lab-only A/B: 0 pipelined (default), 1-3 one-shot modes
-            const char *e = std::getenv("SMFV_TILED_ABLATE");
+    if (!plan->tiled || pick_vec(d_X, ldx, d_Y, ldy, K) != 2)
+        return smfv_spmm_csr_f64(plan->variant, m, plan->n, plan->nnz, d_row_ptr, d_col_idx, d_values,
+                                 d_X, ldx, K, d_Y, ldy, plan->ws, plan->ws_bytes, stream);
+    SMFV_REQUIRE(d_row_ptr && d_X && d_Y && d_values, "null argument");
+    if (d_values != plan->bound_values) {
+        set_error("tiled plan: values not bound (call smfv_plan_bind_values with these d_values)");
+        return SMFV_ERR_INVALID;
+    }
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
+    }
+    if (plan->ntiles > 0) {
+        // one persistent block per CU; a multiple of 8 (>= 8) so every XCD's tile range has blocks
+        const int blocks = std::max(8, (std::min(plan->ntiles, ncu) + 7) & ~7);
+        static const int abl = [] {  // lab-only ablations (k_rows_ws ABL modes)
+            const char *e = std::getenv("SMFV_WS_ABL");
             return e ? std::atoi(e) : 0;
         }();
-        int dev = 0, ncu = 256;
-        if (hipGetDevice(&dev) == hipSuccess) {
-            int v = 0;
-            if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-                ncu = v;
-        }
-        if (plan->kind == 0) {
-            // one persistent block per CU; a multiple of 8 (>= 8) so every XCD's tile range has blocks
-            const int blocks = std::max(8, (std::min(plan->ntiles, ncu) + 7) & ~7);
-            if (plan->ntiles > 0) {
-                static const int abl = [] {
-                    const char *e = std::getenv("SMFV_WS_ABL");
-                    return e ? std::atoi(e) : 0;
-                }();
-                hipLaunchKernelGGL(abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3>
-                                   : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : k_rows_ws<0>, dim3((unsigned)blocks), dim3(1024), 0, as_stream(stream), plan->ntiles,
-                                   K / TILE_KP, plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx,
-                                   d_Y, ldy);
-                SMFV_LAUNCHED();
-            }
-            if (plan->ndirect > 0) {
-                SMFV_REQUIRE(d_col_idx, "null col_idx");
-                hipLaunchKernelGGL(k_rows_list, dim3((unsigned)((plan->ndirect + 31) / 32), (unsigned)(K / TILE_KP)),
-                                   dim3(256), 0, as_stream(stream), plan->ndirect, plan->direct_rows, d_row_ptr,
-                                   d_col_idx, d_values, d_X, ldx, d_Y, ldy);
-                SMFV_LAUNCHED();
-            }
-            return SMFV_OK;
-        }
-        if (ablate == 0 || ablate >= 4) {
-            // 3 x 44 KiB of LDS per CU; a multiple of 8 (>= 8): every XCD's tile range has blocks
-            const int blocks = std::max(8, (std::min(plan->ntiles, 3 * ncu) + 7) & ~7);
-            // lab: 4 masked batches of 8, 5 no compute, 6 no prefetch of X / CSR,
-            // 7 pipelined batches, 8 pipelined batches without prefetch, 9 skeleton
-            auto kern = ablate == 4 ? k_rows_pipe<1, 0> : ablate == 5 ? k_rows_pipe<0, 1>
-                      : ablate == 6 ? k_rows_pipe<0, 2> : ablate == 7 ? k_rows_pipe<2, 0>
-                      : ablate == 8 ? k_rows_pipe<2, 2> : ablate == 9 ? k_rows_pipe<0, 3> : k_rows_pipe<0, 0>;
-            static const int interleave = [] {  // lab: SMFV_TILE_ORDER=0 contiguous runs
-                const char *e = std::getenv("SMFV_TILE_ORDER");
-                return e ? std::atoi(e) : 1;
-            }();
-            hipLaunchKernelGGL(kern, dim3((unsigned)blocks, (unsigned)(K / TILE_KP)), dim3(256),
-                               0, as_stream(stream), plan->ntiles, plan->rec, plan->tlidx, plan->tvals,
-                               d_row_ptr, d_col_idx, d_values, d_X, ldx, K, d_Y, ldy, interleave, nullptr);
-        } else {
-            auto kern = ablate == 2 ? k_rows_tiled<1> : ablate == 3 ? k_rows_tiled<2> : k_rows_tiled<0>;  // 1 one-shot, 2 stage only, 3 compute only
-            hipLaunchKernelGGL(kern, dim3((unsigned)plan->ntiles, (unsigned)(K / TILE_KP)),
-                               dim3(256), 0, as_stream(stream), plan->meta, plan->trows, plan->rbeg,
-                               plan->ucols, plan->tlidx, plan->tvals, d_row_ptr, d_col_idx, d_values,
-                               d_X, ldx, K, d_Y, ldy);
-        }
+        auto kern = abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3>
+                  : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : k_rows_ws<0>;
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, as_stream(stream), plan->ntiles, K / TILE_KP,
+                           plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();
-        return SMFV_OK;
     }
-    return smfv_spmm_csr_f64(plan->variant, m, plan->n, plan->nnz, d_row_ptr, d_col_idx, d_values,
-                             d_X, ldx, K, d_Y, ldy, plan->ws, plan->ws_bytes, stream);
+    if (plan->ndirect > 0) {
+        SMFV_REQUIRE(d_col_idx, "null col_idx");
+        hipLaunchKernelGGL(k_rows_list, dim3((unsigned)((plan->ndirect + 31) / 32), (unsigned)(K / TILE_KP)),
+                           dim3(256), 0, as_stream(stream), plan->ndirect, plan->direct_rows, d_row_ptr, d_col_idx,
+                           d_values, d_X, ldx, d_Y, ldy);
+        SMFV_LAUNCHED();
+    }
+    return SMFV_OK;
 }
 
 SMFV_API int smfv_spmm_rowblock_f64(int row_begin, int row_end, int n, const int *d_row_ptr,

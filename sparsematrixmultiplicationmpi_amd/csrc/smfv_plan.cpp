@@ -111,20 +111,12 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A, 
                 break;
             add_row(best);
         }
-        // rows by decreasing length: the 8 rows of a wave (one per 8-lane
-        // team) have similar lengths, so less of the wave idles on the
-        // longest row (lane-slot waste 25% -> 15% on the cop20k_A surrogate)
-        static const bool by_index = [] {  // lab toggle: SMFV_TILE_SORT=index
-            const char *e = std::getenv("SMFV_TILE_SORT");
-            return e && std::string(e) == "index";
-        }();
-        if (by_index)
-            std::sort(rows.begin(), rows.end());
-        else
-            std::sort(rows.begin(), rows.end(), [&](int a, int b) {
-                const int la = rp[a + 1] - rp[a], lb = rp[b + 1] - rp[b];
-                return la != lb ? la > lb : a < b;
-            });
+        // rows by decreasing length (build_ws_plan deals them to waves in
+        // this order, so the rows of a wave have similar lengths)
+        std::sort(rows.begin(), rows.end(), [&](int a, int b) {
+            const int la = rp[a + 1] - rp[a], lb = rp[b + 1] - rp[b];
+            return la != lb ? la > lb : a < b;
+        });
 
         TileMeta tm{};
         tm.roff = (int)A.trows.size();
@@ -169,25 +161,6 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A, 
         A.meta.push_back(tm);
         ++tile;
     }
-}
-
-std::vector<int> pack_tile_records(const TileAnalysis &A)
-{
-    std::vector<int> rec(A.meta.size() * TREC_WORDS, 0);
-    for (size_t t = 0; t < A.meta.size(); ++t) {
-        int *r = rec.data() + t * TREC_WORDS;
-        const TileMeta &tm = A.meta[t];
-        static_assert(sizeof(TileMeta) == 8 * sizeof(int), "TileMeta is 8 words");
-        std::memcpy(r, &tm, sizeof tm);
-        for (int k = 0; k < tm.nrows; ++k) {
-            r[TREC_ROWS + k] = A.trows[tm.roff + k];
-            r[TREC_INFO + k] = A.rbeg[tm.roff + k];
-        }
-        // union id u at (u % 16) * 8 + u / 16: the staging thread for rows
-        // u = xr + 16k finds its 8 ids contiguous
-        for (int u = 0; u < tm.nu; ++u) r[TREC_UCOLS + (u % 16) * 8 + u / 16] = A.ucols[tm.uoff + u];
-    }
-    return rec;
 }
 
 // ---------------------------------------------------------------------------
@@ -262,13 +235,8 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
 bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::string *err)
 {
     P = WsPlan();
-    TileCaps caps;
-    caps.ucap = WS_UCAP;
-    caps.ncap = WS_NCAP - 192;  // leaves room for the quads' interleave padding
-    caps.maxrows = WS_ROWS;
-    caps.pad = 8;
     TileAnalysis T;
-    analyse_tiles(m, n, rp, ci, T, caps);
+    analyse_tiles(m, n, rp, ci, T);  // TileCaps defaults are the k_rows_ws caps
 
     auto len8 = [&](int r) { return std::max(8, (rp[r + 1] - rp[r] + 7) & ~7); };
     // entries of a row set sorted by decreasing length: a quad takes 4x its first (longest) row
