@@ -15,11 +15,13 @@
 #include <hip/hip_runtime.h>
 #include <mpi.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "SparseMatrixFatVectorMultiply.h"
@@ -101,53 +103,107 @@ smfv_comm_t comm_world()
     return c.comm;
 }
 
-template <class T> struct DevBuf {
-    T *p = nullptr;
-    explicit DevBuf(size_t n)
+// Buffers reused across calls (grow-only): the device copies of A, X, Y and
+// the workspace, and pinned host staging for X (in) and Y (out), so a call
+// pays no hipMalloc and its X / Y transfers run at pinned-copy speed
+// (the FatVector <-> flat conversion and the rank-0
+// rebuild are a large share of the reference's RowWise time).
+struct Cached {
+    void *p = nullptr;
+    size_t cap = 0;
+    bool pinned = false;
+    void *get(size_t bytes)
     {
-        if (n) hip_check(hipMalloc(reinterpret_cast<void **>(&p), n * sizeof(T)), "hipMalloc");
+        if (bytes <= cap) return p;
+        release();
+        const size_t b = std::max<size_t>(bytes, 256);
+        if (pinned)
+            hip_check(hipHostMalloc(&p, b, hipHostMallocDefault), "hipHostMalloc");
+        else
+            hip_check(hipMalloc(&p, b), "hipMalloc");
+        cap = b;
+        return p;
     }
-    ~DevBuf()
+    void release()
     {
-        if (p) (void)hipFree(p);
+        if (p) (void)(pinned ? hipHostFree(p) : hipFree(p));
+        p = nullptr;
+        cap = 0;
     }
-    DevBuf(const DevBuf &) = delete;
-    DevBuf &operator=(const DevBuf &) = delete;
 };
+
+struct Buffers {
+    Cached rp, ci, va, X, Y, ws, hX{nullptr, 0, true}, hY{nullptr, 0, true};
+};
+
+Buffers &bufs()
+{
+    static Buffers *b = new Buffers;  // process lifetime (freed with the context at exit)
+    return *b;
+}
+
+// host rows [0, rows) copied in parallel (plain threads: the copies are
+// memory-bound and the FatVector side is m separate allocations)
+template <class F> void par_rows(int rows, F f)
+{
+    const int nt = rows < 4096 ? 1 : (int)std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency()));
+    if (nt == 1) {
+        f(0, rows);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t) th.emplace_back(f, (int)((int64_t)rows * t / nt), (int)((int64_t)rows * (t + 1) / nt));
+    for (auto &x : th) x.join();
+}
 
 // A and X resident on the device for one call
 struct Problem {
     int m, n, K;
     int64_t nnz;
-    DevBuf<int> rp, ci;
-    DevBuf<double> va, X, Y;
+    int *rp, *ci;
+    double *va, *X, *Y;
     Problem(const SparseMatrix &A, const FatVector &fat, int K_, hipStream_t st)
-        : m(A.numRows), n(A.numCols), K(K_), nnz((int64_t)A.values.size()), rp(A.rowPtr.size()),
-          ci(A.colIndices.size()), va(A.values.size()), X((size_t)A.numCols * K_),
-          Y((size_t)A.numRows * K_)
+        : m(A.numRows), n(A.numCols), K(K_), nnz((int64_t)A.values.size())
     {
         if ((int)A.rowPtr.size() != m + 1 || (int64_t)A.colIndices.size() != nnz ||
             (m >= 0 && A.rowPtr.size() && A.rowPtr[m] != nnz))
             fail("malformed SparseMatrix (rowPtr / colIndices / values sizes)");
         if ((int)fat.size() != n) fail("fatVector has " + std::to_string(fat.size()) + " rows, matrix has " + std::to_string(n) + " columns");
-        std::vector<double> flat = serialize(fat);
-        if ((int64_t)flat.size() != (int64_t)n * K) fail("fatVector rows must have vecCols entries");
-        auto up = [&](void *d, const void *h, size_t b) {
-            if (b) hip_check(hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+        for (const auto &r : fat)
+            if ((int)r.size() != K) fail("fatVector rows must have vecCols entries");
+        Buffers &B = bufs();
+        rp = static_cast<int *>(B.rp.get(A.rowPtr.size() * sizeof(int)));
+        ci = static_cast<int *>(B.ci.get(A.colIndices.size() * sizeof(int)));
+        va = static_cast<double *>(B.va.get(A.values.size() * sizeof(double)));
+        X = static_cast<double *>(B.X.get((size_t)n * K * sizeof(double)));
+        Y = static_cast<double *>(B.Y.get((size_t)m * K * sizeof(double)));
+        // serialize (SC/utils.cpp:216-228) straight into pinned staging
+        double *hx = static_cast<double *>(B.hX.get((size_t)n * K * sizeof(double)));
+        par_rows(n, [&](int a, int b) {
+            for (int i = a; i < b; ++i) std::copy(fat[i].begin(), fat[i].end(), hx + (size_t)i * K);
+        });
+        auto up = [&](void *d, const void *h, size_t bytes) {
+            if (bytes) hip_check(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
         };
-        up(rp.p, A.rowPtr.data(), A.rowPtr.size() * sizeof(int));
-        up(ci.p, A.colIndices.data(), A.colIndices.size() * sizeof(int));
-        up(va.p, A.values.data(), A.values.size() * sizeof(double));
-        up(X.p, flat.data(), flat.size() * sizeof(double));
+        up(rp, A.rowPtr.data(), A.rowPtr.size() * sizeof(int));
+        up(ci, A.colIndices.data(), A.colIndices.size() * sizeof(int));
+        up(va, A.values.data(), A.values.size() * sizeof(double));
+        up(X, hx, (size_t)n * K * sizeof(double));
     }
+    void *workspace(size_t bytes) { return bytes ? bufs().ws.get(bytes) : nullptr; }
     FatVector download(hipStream_t st)
     {
-        std::vector<double> flat((size_t)m * K);
-        if (!flat.empty())
-            hip_check(hipMemcpyAsync(flat.data(), Y.p, flat.size() * sizeof(double), hipMemcpyDeviceToHost, st),
+        double *hy = static_cast<double *>(bufs().hY.get((size_t)m * K * sizeof(double)));
+        if ((size_t)m * K)
+            hip_check(hipMemcpyAsync(hy, Y, (size_t)m * K * sizeof(double), hipMemcpyDeviceToHost, st),
                       "hipMemcpyAsync");
         hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
-        return deserialize(flat, m, K);
+        // deserialize (SC/utils.cpp:238-253): the m row vectors built in parallel
+        FatVector out((size_t)m);
+        par_rows(m, [&](int a, int b) {
+            for (int i = a; i < b; ++i) out[i].assign(hy + (size_t)i * K, hy + (size_t)(i + 1) * K);
+        });
+        return out;
     }
 };
 
@@ -157,9 +213,8 @@ FatVector local_run(int variant, const SparseMatrix &A, const FatVector &fat, in
     Problem P(A, fat, K, c.stream);
     size_t wsb = 0;
     check(smfv_spmm_workspace_bytes(variant, P.m, P.nnz, K, &wsb), "smfv_spmm_workspace_bytes");
-    DevBuf<char> ws(wsb);
-    check(smfv_spmm_csr_f64(variant, P.m, P.n, P.nnz, P.rp.p, P.ci.p, P.va.p, P.X.p, K, K, P.Y.p, K,
-                            ws.p, wsb, c.stream),
+    check(smfv_spmm_csr_f64(variant, P.m, P.n, P.nnz, P.rp, P.ci, P.va, P.X, K, K, P.Y, K, P.workspace(wsb), wsb,
+                            c.stream),
           "smfv_spmm_csr_f64");
     return P.download(c.stream);
 }
@@ -173,9 +228,8 @@ FatVector collective_run(int variant, const SparseMatrix &A, const FatVector &fa
     size_t wsb = 0;
     check(smfv_dist_workspace_bytes(comm, variant, P.m, P.nnz, A.rowPtr.data(), K, &wsb),
           "smfv_dist_workspace_bytes");
-    DevBuf<char> ws(wsb);
-    check(smfv_dist_spmm_f64(comm, variant, SMFV_TO_ROOT, 0, P.m, P.n, P.nnz, A.rowPtr.data(), P.rp.p,
-                             P.ci.p, P.va.p, P.X.p, K, P.Y.p, ws.p, wsb, c.stream),
+    check(smfv_dist_spmm_f64(comm, variant, SMFV_TO_ROOT, 0, P.m, P.n, P.nnz, A.rowPtr.data(), P.rp, P.ci,
+                             P.va, P.X, K, P.Y, P.workspace(wsb), wsb, c.stream),
           "smfv_dist_spmm_f64");
     if (c.rank != 0) {
         hip_check(hipStreamSynchronize(c.stream), "hipStreamSynchronize");

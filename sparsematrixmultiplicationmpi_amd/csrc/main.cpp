@@ -89,6 +89,12 @@ void run_vendor(const SparseMatrix &M, const FatVector &v, int k, const FatVecto
          hipMemcpy(X, flat.data(), flat.size() * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
     smfv_vendor_t h = nullptr;
     double t0 = 0, t1 = 0;
+    if (ok) {  // untimed warm-up: rocSPARSE's handle and kernel loading are one-time costs
+        ok = smfv_vendor_spmm_create(&h, 0, m, n, nnz, rp, ci, va, X, k, k, Y, k, nullptr) == SMFV_OK &&
+             smfv_vendor_spmm_execute(h) == SMFV_OK && hipDeviceSynchronize() == hipSuccess;
+        if (h) smfv_vendor_spmm_destroy(h);
+        h = nullptr;
+    }
     if (ok) {
         t0 = MPI_Wtime();
         ok = smfv_vendor_spmm_create(&h, 0, m, n, nnz, rp, ci, va, X, k, k, Y, k, nullptr) == SMFV_OK &&
@@ -137,6 +143,10 @@ int main(int argc, char *argv[])
         std::cout << "Matrix size: " << M.numRows << "x" << M.numCols << std::endl;
         v = generateLargeFatVector(M.numCols, k);
         std::cout << "Vector size: " << M.numCols << "x" << k << std::endl;
+        // one untimed call first: HIP context, code-object load and the
+        // library's buffer cache are one-time costs, not the algorithm's
+        // (the reference's CPU loop has none); the timed call does all the work
+        (void)sparseMatrixFatVectorMultiply(M, v, k);
         const double t0 = MPI_Wtime();
         serial = sparseMatrixFatVectorMultiply(M, v, k);
         const double t1 = MPI_Wtime();
