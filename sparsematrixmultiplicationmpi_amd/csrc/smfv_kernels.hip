@@ -384,7 +384,8 @@ __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(
 // only (every unit recomputes the first staged tile), 3 as 2 without Y stores,
 // 4 as 2 without the per-unit barriers (waves run their units unsynchronised),
 // 5 staging and compute both running, decoupled (no barriers; compute reads
-// slot 0 while it is restaged: timing only, results are garbage)
+// slot 0 while it is restaged: timing only, results are garbage), 6 as 2 with
+// half the X reads (the other half synthesised by a multiply; timing only)
 template <int ABL>
 __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
@@ -463,7 +464,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
         int it = 0, p = 0;  // unit u + 1 to stage
         if (++p == npanel) p = 0, ++it;
         for (int u = 0; u < nunits; ++u) {
-            if (u + 1 < nunits && ABL != 2 && ABL != 3 && ABL != 4) {
+            if (u + 1 < nunits && ABL != 2 && ABL != 3 && ABL != 4 && ABL != 6) {
                 const int t = t0 + it * tstep;
                 stage(t, p, (u + 1) & 1, it & 1);
                 if (p == npanel - 1) fetch_record(min(t + tstep, tlast));
@@ -481,7 +482,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
     barrier_lds();
     int it = 0, p = 0;
     for (int u = 0; u < nunits; ++u) {
-        // (ABL 2 / 3 recompute the prologue's unit: slot 0 is the only staged one)
+        // (ABL >= 2 recompute the prologue's unit: slot 0 is the only staged one)
         const char *xbase = lds + (ABL >= 2 ? 0 : (u & 1)) * XSLOT;
         const char *mbase = lds + SL_M + (ABL >= 2 ? 0 : (it & 1)) * MSLOT;
         const int *R = reinterpret_cast<const int *>(mbase + M_R);
@@ -500,9 +501,14 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
             // half's LDS latency hides behind the other half's FP64 work
             auto rdx = [&](unsigned w, d2 &a0, d2 &a1, d2 &b0, d2 &b1) {
                 a0 = *reinterpret_cast<const d2 *>(xb0 + (w & 0xFFFF));
-                a1 = *reinterpret_cast<const d2 *>(xb1 + (w & 0xFFFF));
                 b0 = *reinterpret_cast<const d2 *>(xb0 + (w >> 16));
-                b1 = *reinterpret_cast<const d2 *>(xb1 + (w >> 16));
+                if constexpr (ABL == 6) {  // lab: half the X reads (timing only)
+                    a1 = a0 * 1.5;
+                    b1 = b0 * 1.5;
+                } else {
+                    a1 = *reinterpret_cast<const d2 *>(xb1 + (w & 0xFFFF));
+                    b1 = *reinterpret_cast<const d2 *>(xb1 + (w >> 16));
+                }
             };
             u4 ln = Lq[0];
             d2 vn[4];
@@ -1411,7 +1417,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             return e ? std::atoi(e) : 0;
         }();
         auto kern = abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3>
-                  : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : k_rows_ws<0>;
+                  : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : abl == 6 ? k_rows_ws<6> : k_rows_ws<0>;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, as_stream(stream), plan->ntiles, K / TILE_KP,
                            plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();
