@@ -343,6 +343,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rows", type=int, default=0, help="syn80m_k32: matrix rows (default 80M)")
     ap.add_argument("--no-vendor", action="store_true", help="skip the rocSPARSE comparator leg")
+    ap.add_argument("--fma", action="store_true",
+                    help="time the opt-in FMA plans (SMFV_PLAN_FMA) instead of the bit-exact ones")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -395,7 +397,7 @@ def main() -> None:
             dX = torch.empty((n, K), dtype=torch.float64, device=dev)
             smfv.fill_x_hash(dX, 43)
         dY = torch.empty((m, K), dtype=torch.float64, device=dev)
-        copies.append((smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles), dX, dY))
+        copies.append((smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles, fma=args.fma), dX, dY))
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
 

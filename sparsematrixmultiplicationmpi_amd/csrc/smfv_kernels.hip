@@ -386,7 +386,7 @@ __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(
 // 5 staging and compute both running, decoupled (no barriers; compute reads
 // slot 0 while it is restaged: timing only, results are garbage), 6 as 2 with
 // half the X reads (the other half synthesised by a multiply; timing only)
-template <int ABL>
+template <int ABL, bool FMA = false>
 __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
                                                      const uint16_t *__restrict__ loff,
@@ -476,6 +476,14 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
         return;
     }
     // ---------------- compute waves ----------------
+    // FMA (opt-in plan flag SMFV_PLAN_FMA): one fused multiply-add per term,
+    // within the reference's 1e-6 tolerance but no longer bit-identical
+    auto madd = [](d2 a, double v, d2 x) -> d2 {
+        if constexpr (FMA)
+            return d2{__builtin_fma(v, x.x, a.x), __builtin_fma(v, x.y, a.y)};
+        else
+            return a + v * x;
+    };
     const int tw = (tid >> 3) & 7, tl = tid & 7, par = tw & 1;
     const int slot = tw * 8 + wv;
     const int qk = tw & 3;  // position of the team in its quad
@@ -531,16 +539,16 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
                     vn[q] = *(const volatile __attribute__((address_space(3))) d2 *)(Vq + 4 * (4 * bn + q));
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    acc0 = acc0 + v[k] * xa0[k];
-                    acc1 = acc1 + v[k] * xa1[k];
+                    acc0 = madd(acc0, v[k], xa0[k]);
+                    acc1 = madd(acc1, v[k], xa1[k]);
                 }
                 rdx(ln.x, xa0[0], xa1[0], xa0[1], xa1[1]);  // first half of batch b + 1
                 rdx(ln.y, xa0[2], xa1[2], xa0[3], xa1[3]);
                 __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the second half's FP64
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    acc0 = acc0 + v[4 + k] * xc0[k];
-                    acc1 = acc1 + v[4 + k] * xc1[k];
+                    acc0 = madd(acc0, v[4 + k], xc0[k]);
+                    acc1 = madd(acc1, v[4 + k], xc1[k]);
                 }
             }
             double *y = Y + (int64_t)row * ldy + p * TILE_KP + 2 * tl;
@@ -1174,6 +1182,7 @@ constexpr int SMFV_TILE_SAMPLE_ROWS = 16384;  // rows analysed first to estimate
 
 struct smfv_plan_s {
     int variant = 0, m = 0, n = 0, K = 0;
+    bool fma = false;  // SMFV_PLAN_FMA: fused multiply-add in the tiled kernel (not bit-identical)
     int64_t nnz = 0;
     bool tiled = false;
     int ntiles = 0, ndirect = 0;
@@ -1215,6 +1224,7 @@ SMFV_API int smfv_plan_create(smfv_plan_t *out, int variant, int m, int n, int64
     SMFV_REQUIRE(m >= 0 && n >= 0 && nnz >= 0 && nnz <= 0x7fffffff && K >= 0, "bad sizes");
     SMFV_REQUIRE(h_row_ptr == nullptr || h_row_ptr[m] == nnz, "row_ptr[m] != nnz");
     auto *p = new smfv_plan_s;
+    p->fma = (flags & SMFV_PLAN_FMA) != 0;
     p->variant = variant;
     p->m = m;
     p->n = n;
@@ -1416,7 +1426,8 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             const char *e = std::getenv("SMFV_WS_ABL");
             return e ? std::atoi(e) : 0;
         }();
-        auto kern = abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3>
+        auto kern = plan->fma ? (abl == 2 ? k_rows_ws<2, true> : k_rows_ws<0, true>)
+                  : abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3>
                   : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : abl == 6 ? k_rows_ws<6> : k_rows_ws<0>;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, as_stream(stream), plan->ntiles, K / TILE_KP,
                            plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);

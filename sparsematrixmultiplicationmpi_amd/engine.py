@@ -86,7 +86,7 @@ def _check_dense(T: torch.Tensor, rows: int, K: int, name: str) -> int:
     return max(int(T.stride(0)), K)
 
 
-PLAN_NO_TILES, PLAN_FORCE_TILES = 1, 2
+PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA = 1, 2, 4
 
 
 class SpmmPlan:
@@ -95,11 +95,14 @@ class SpmmPlan:
     analysis that lets the kernel stage re-used X rows in LDS.  run() is a
     pure asynchronous launch sequence (capturable into a hipGraph).
 
-    tiles: "auto" (stage when re-use >= 3), "off", or "force"."""
+    tiles: "auto" (stage when re-use >= 3), "off", or "force".  fma: opt-in
+    fused multiply-add in the tiled kernel (SMFV_PLAN_FMA)."""
 
-    def __init__(self, variant: int, A: DeviceCSR, K: int, tiles: str = "auto"):
+    def __init__(self, variant: int, A: DeviceCSR, K: int, tiles: str = "auto", fma: bool = False):
         self.variant, self.A, self.K = Variant(variant), A, K
         flags = {"auto": 0, "off": PLAN_NO_TILES, "force": PLAN_FORCE_TILES}[tiles]
+        if fma:  # opt-in fused multiply-add in the tiled kernel: within tolerance, not bit-identical
+            flags |= PLAN_FMA
         self._plan = ctypes.c_void_p()
         ip = ctypes.POINTER(ctypes.c_int)
         call("smfv_plan_create", byref(self._plan), int(variant), A.m, A.n, A.nnz,

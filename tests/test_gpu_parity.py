@@ -343,3 +343,19 @@ def test_vendor_rocsparse_comparator(gpu, alg):
     scale = oracle.spmm("sequential", A.rowPtr, A.colIndices, np.abs(A.values), np.abs(X))
     assert np.all(np.abs(Yh - Yref) <= 1e-12 * scale + 1e-300)
     assert np.max(np.abs(Yh - Yref)) <= 1e-6
+
+
+def test_tiled_plan_fma_within_tolerance(gpu):
+    """Opt-in SMFV_PLAN_FMA: same per-row order, fused multiply-add; within
+    1e-12 x sum|a||x| of the reference (the north star allows 1e-6 relative)."""
+    A = smfv.gen_fem27(5000, 12, 12, 0.83, 7)
+    K = 64
+    X = np.random.default_rng(7).uniform(-1, 1, (A.numCols, K))
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    scale = oracle.spmm("sequential", A.rowPtr, A.colIndices, np.abs(A.values), np.abs(X))
+    dA = smfv.DeviceCSR(A, gpu)
+    plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles="force", fma=True)
+    Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+    plan.run(torch.from_numpy(X).to(gpu), Y)
+    torch.cuda.synchronize()
+    assert np.all(np.abs(Y.cpu().numpy() - Yref) <= 1e-12 * scale + 1e-300)
