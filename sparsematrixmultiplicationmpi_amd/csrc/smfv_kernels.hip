@@ -497,7 +497,9 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
         const int row = R[slot];
         if (row >= 0 && ABL != 1) {
             const int info = R[64 + slot];
-            const int js = info & 0xFFFF, nbat = (info >> 16) >> 3;
+            // the row runs nbat whole batches of 8, then (half) one of 4
+            const int js = info & 0xFFFF, nh = (info >> 16) >> 2, nbat = nh >> 1, half = nh & 1;
+            const int blast = nbat + half - 1;
             const u4 *Lq = reinterpret_cast<const u4 *>(mbase + M_L) + js + qk;
             const d2 *Vq = reinterpret_cast<const d2 *>(mbase + M_V) + R[128 + slot] + qk;
             const char *xb0 = xbase + par * 128 + tl * 16;
@@ -532,7 +534,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
                 const double v[8] = {vn[0].x, vn[0].y, vn[1].x, vn[1].y, vn[2].x, vn[2].y, vn[3].x, vn[3].y};
                 // next batch's meta (the last batch re-reads itself); volatile
                 // keeps these reads here, behind this batch's X reads
-                const int bn = min(b + 1, nbat - 1);
+                const int bn = min(b + 1, blast);
                 ln = *(const volatile __attribute__((address_space(3))) u4 *)(Lq + 4 * bn);
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
@@ -549,6 +551,14 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
                 for (int k = 0; k < 4; ++k) {
                     acc0 = madd(acc0, v[4 + k], xc0[k]);
                     acc1 = madd(acc1, v[4 + k], xc1[k]);
+                }
+            }
+            if (half) {  // xa / vn hold the first half of batch blast: its 4 entries end the row
+                const double v[4] = {vn[0].x, vn[0].y, vn[1].x, vn[1].y};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    acc0 = madd(acc0, v[k], xa0[k]);
+                    acc1 = madd(acc1, v[k], xa1[k]);
                 }
             }
             double *y = Y + (int64_t)row * ldy + p * TILE_KP + 2 * tl;

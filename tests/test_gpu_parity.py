@@ -324,6 +324,29 @@ def test_tiled_plan_tiny(gpu, name, K):
     assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref))
 
 
+@pytest.mark.parametrize("K", [32, 128])
+def test_tiled_plan_every_row_length(gpu, K):
+    """Row lengths 0..40 (every residue mod 8: rows ending on a half batch of
+    4 entries, on a whole batch of 8, or both) in forced tiles, columns from a
+    local window so rows share X rows; bit-identical to the reference order."""
+    rng = np.random.default_rng(7 + K)
+    m = n = 3000
+    lens = np.arange(m) % 41
+    rp = np.zeros(m + 1, np.int32)
+    rp[1:] = np.cumsum(lens)
+    ci = np.concatenate([np.sort(rng.choice(np.arange(max(0, i - 60), min(n, i + 60)), L, replace=False))
+                         for i, L in enumerate(lens)]).astype(np.int32)
+    A = smfv.SparseMatrix(values=rng.uniform(-1, 1, ci.size), colIndices=ci, rowPtr=rp, numRows=m, numCols=n)
+    X = rng.uniform(-1, 1, (n, K))
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(A, gpu), K, tiles="force")
+    assert plan.stats()["tiled"]
+    Y = torch.full((m, K), np.nan, dtype=torch.float64, device=gpu)
+    plan.run(torch.from_numpy(X).to(gpu), Y)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref))
+
+
 @pytest.mark.parametrize("alg", [0, 1, 2])
 def test_vendor_rocsparse_comparator(gpu, alg):
     """The rocSPARSE comparator (PETSc-block analogue) agrees with the
