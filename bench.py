@@ -76,6 +76,8 @@ def kernel_label(variant: str, K: int, plan_stats: dict) -> str:
         return "k_merge_flat + k_carry_fixup" if K % 32 == 0 else "k_merge + k_carry_fixup"
     if plan_stats.get("tiled"):
         return "k_rows_ws"
+    if K == 1:
+        return "k_spmv_stream<256, 64, 2048>"
     if K % 2:
         return "k_rows<TEAM,1>"
     pairs = K // 2

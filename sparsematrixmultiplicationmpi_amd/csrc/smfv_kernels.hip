@@ -198,6 +198,66 @@ __global__ __launch_bounds__(256) void k_rows(int row_begin, int nrows, const in
 }
 
 // ---------------------------------------------------------------------------
+// k_spmv_stream: K = 1 (SpMV, BASELINE config 1 on the GPU).  One lane per
+// row, RPB consecutive rows per NT-lane block.  The block's non-zeros are streamed in
+// chunks of CH: every lane loads CH / NT (col, val) pairs with coalesced
+// loads, gathers X (n doubles, L2-resident for cop20k) and writes the
+// products a_j * x_j to LDS; then each lane adds its row's products of the
+// chunk in CSR order, carrying the partial sum across chunks.  The product
+// is rounded before the add exactly as in the reference's y += a * x
+// (SC/SparseMatrixFatVectorMultiply.cpp:22-24), so the result is
+// bit-identical.
+// ---------------------------------------------------------------------------
+template <int NT, int RPB, int CH>
+__global__ __launch_bounds__(NT) void k_spmv_stream(int row_begin, int nrows, const int *__restrict__ rp,
+                                                    const int *__restrict__ ci,
+                                                    const double *__restrict__ va,
+                                                    const double *__restrict__ X, int64_t ldx,
+                                                    double *__restrict__ Y, int64_t ldy)
+{
+    static_assert(CH % NT == 0 && RPB <= NT, "whole products per lane, one lane per row");
+    constexpr int PER = CH / NT;
+    __shared__ double prod[CH];
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int lr0 = blk * RPB;
+    const int nr = min(RPB, nrows - lr0);
+    if (nr <= 0) return;  // block-uniform
+    const int r0 = row_begin + lr0, t = threadIdx.x;
+    const int e0 = rp[r0], e1 = rp[r0 + nr];
+    int js = 0, je = 0;
+    if (t < nr) js = rp[r0 + t], je = rp[r0 + t + 1];
+    double acc = 0.0;
+    for (int64_t c0 = e0; c0 < e1; c0 += CH) {  // (int64: c0 + CH may pass INT_MAX)
+        const int cn = (int)min((int64_t)CH, (int64_t)e1 - c0);
+        int c[PER];
+        double v[PER], x[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = t + i * NT;
+            c[i] = e < cn ? __builtin_nontemporal_load(ci + c0 + e) : 0;
+            v[i] = e < cn ? __builtin_nontemporal_load(va + c0 + e) : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < PER; ++i) x[i] = t + i * NT < cn ? X[(int64_t)c[i] * ldx] : 0.0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) prod[t + i * NT] = v[i] * x[i];
+        __syncthreads();
+        int j = (int)(max((int64_t)js, c0) - c0);
+        const int b = (int)(min((int64_t)je, c0 + cn) - c0);
+        for (; j + 4 <= b; j += 4) {
+            const double p0 = prod[j], p1 = prod[j + 1], p2 = prod[j + 2], p3 = prod[j + 3];
+            acc = acc + p0;
+            acc = acc + p1;
+            acc = acc + p2;
+            acc = acc + p3;
+        }
+        for (; j < b; ++j) acc = acc + prod[j];
+        __syncthreads();
+    }
+    if (t < nr) Y[(int64_t)(lr0 + t) * ldy] = acc;
+}
+
+// ---------------------------------------------------------------------------
 // k_rows_mh: the production row kernel for K even and 16-byte aligned X/Y.
 //
 //  * a block of 256 lanes owns 256/TEAM consecutive rows; it stages its
@@ -1017,6 +1077,19 @@ static int launch_rows(int row_begin, int nrows, const int *rp, const int *ci, c
                        hipStream_t st)
 {
     if (nrows <= 0 || K <= 0) return SMFV_OK;
+    if (K == 1) {  // SpMV: coalesced CSR stream, products staged in LDS
+        // 64 rows / 2,048-entry chunk per 256-lane block: one chunk per block
+        // on cop20k (~1,390 non-zeros), 1,894 blocks.  Block-shape sweep on
+        // the surrogate (cold us): 256 rows 19.5, 128 rows 12.6, 64 rows
+        // 10.4-10.5, 32 rows 10.6-11.4, 512 lanes x 128 rows 10.4
+        constexpr int NT = 256, RPB = 64, CH = 2048;
+        const int64_t nblk = ((int64_t)nrows + RPB - 1) / RPB;
+        SMFV_REQUIRE(nblk <= 0x7fffffff, "too many rows for one launch");
+        hipLaunchKernelGGL((k_spmv_stream<NT, RPB, CH>), dim3((unsigned)nblk), dim3(NT), 0, st, row_begin, nrows,
+                           rp, ci, va, X, ldx, Y, ldy);
+        SMFV_LAUNCHED();
+        return SMFV_OK;
+    }
     const int vec = pick_vec(X, ldx, Y, ldy, K);
     if (vec == 2) return launch_rows_mh(row_begin, nrows, rp, ci, va, X, ldx, xrows, K, Y, ldy, st);
     // odd K or unaligned X / Y: one double per lane, shuffle-broadcast kernel

@@ -382,3 +382,27 @@ def test_tiled_plan_fma_within_tolerance(gpu):
     plan.run(torch.from_numpy(X).to(gpu), Y)
     torch.cuda.synchronize()
     assert np.all(np.abs(Y.cpu().numpy() - Yref) <= 1e-12 * scale + 1e-300)
+
+
+def test_spmv_stream_k1(gpu):
+    """K = 1 (k_spmv_stream): rows spanning many 2048-entry chunks, empty
+    rows, a row block that starts mid-matrix and an unaligned leading
+    dimension; bit-identical to the reference order."""
+    m, n = 700, 50000
+    lens = np.random.default_rng(11).integers(0, 40, m)
+    lens[[3, 300]] = [9000, 20000]
+    lens[[0, 1, 699]] = 0
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    rng = np.random.default_rng(12)
+    ci = np.concatenate([np.sort(rng.choice(n, L, replace=False)) for L in lens]).astype(np.int32)
+    A = mat(rp, ci, rng.uniform(-1, 1, rp[-1]), m, n)
+    X = rng.uniform(-1, 1, (n, 1))
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    for v in (smfv.Variant.SEQUENTIAL, smfv.Variant.ROWWISE, smfv.Variant.COLUMNWISE):
+        assert np.array_equal(bits(run(v, A, X, gpu)), bits(Yref)), v
+        assert np.array_equal(bits(run(v, A, X, gpu, 1, 3)), bits(Yref)), v
+    dA = smfv.DeviceCSR(A, gpu)
+    Y = torch.full((m, 1), np.nan, dtype=torch.float64, device=gpu)
+    S.spmm_rowblock(dA, 250, 650, torch.from_numpy(X).to(gpu), Y[250:650])
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(Y[250:650].cpu().numpy()), bits(Yref[250:650]))
