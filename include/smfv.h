@@ -83,6 +83,12 @@ SMFV_API void smfv_partition_cols(int K, int p, int r, int *start, int *end);
 SMFV_API void smfv_partition_nnz(int64_t nnz, int p, int r, int64_t *start, int64_t *end);
 
 /* ---- single-device SpMM ------------------------------------------------- */
+/* Merge-path geometry of SMFV_NONZERO over nrows rows / nnz non-zeros
+ * (host): out[0] merge items (rows + non-zeros), [1] items per team, [2]
+ * teams.  Team t walks diagonals [t * out[1], (t + 1) * out[1]); a row open at
+ * a team boundary is finished by the carry fix-up (tests sample those rows). */
+SMFV_API int smfv_merge_geometry(int nrows, int64_t nnz, int K, int64_t out[3]);
+
 /* Device workspace (bytes) smfv_spmm_csr_f64 needs for `variant`; 0 for all
  * but SMFV_NONZERO (merge-path carry slots). */
 SMFV_API int smfv_spmm_workspace_bytes(int variant, int m, int64_t nnz, int K, size_t *bytes);
@@ -99,17 +105,28 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz,
  * The plan owns all device workspace (merge-path carries for NONZERO) and,
  * for SEQUENTIAL / ROWWISE / COLUMNWISE with K a multiple of 32, a clustered
  * row-tile analysis of the pattern (h_col_idx needed): tiles of <= 64 rows
- * grown by adjacency whose distinct X rows (<= 255) fit a 64 KiB LDS image,
+ * grown by adjacency whose distinct X rows (<= 239) fit a 60 KiB LDS image,
  * with a tile-ordered copy of the values and 16-bit X-row offsets.  The tiled
  * kernel (one warp-specialised block per CU, double-buffered LDS-DMA staging)
  * stages each tile's X rows once and reads them from LDS -- same per-row
  * order and arithmetic, bit-identical result; rows over a cap alone are
- * gathered straight from X by a second launch.  Tiling is used when
- * the re-use (non-zeros per staged X row) is >= 3 or SMFV_PLAN_FORCE_TILES
- * is set.  A tiled plan must be bound to A's device values with
- * smfv_plan_bind_values (and re-bound after they change); execute checks
- * that it is given the bound pointer.  Creation allocates device memory and
- * synchronises; bind and execute are asynchronous and graph-capturable. */
+ * gathered straight from X by a second launch.  Tiling is used when the
+ * re-use (non-zeros per staged X row) is >= 3 -- estimated first on 512 tiles
+ * grown in the full pattern, so the decision does not depend on the row
+ * numbering -- or when SMFV_PLAN_FORCE_TILES is set.
+ *
+ * Values contract of a TILED plan: smfv_plan_bind_values gathers a snapshot
+ * of A's device values (tile order, and the directly-gathered rows) and the
+ * plan computes with that snapshot until the next bind.  After the values
+ * change -- at the same address or not -- the caller must bind again;
+ * execute refuses a d_values pointer other than the bound one.  Untiled plans
+ * read the live values.  The pattern (row_ptr / col_idx) must not change over
+ * a plan's life.
+ *
+ * Streams: create allocates device memory and synchronises; bind and execute
+ * are asynchronous and graph-capturable.  An execute on a stream other than
+ * the bind's waits for the bind's gather (hipStreamWaitEvent; while capturing
+ * it requires the gather to have completed).  A plan is not thread-safe. */
 typedef struct smfv_plan_s *smfv_plan_t;
 #define SMFV_PLAN_NO_TILES 1
 #define SMFV_PLAN_FORCE_TILES 2
@@ -120,6 +137,13 @@ typedef struct smfv_plan_s *smfv_plan_t;
 #define SMFV_PLAN_FMA 4
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
+/* Plan of the row block [row_begin, row_end) of a CSR matrix (h_row_ptr /
+ * h_col_idx: host arrays of the WHOLE matrix; the analysis runs on the
+ * block's own rows): what one rank of SC/...RowWise.cpp:36-50 computes.
+ * Execute takes the whole matrix's device arrays and writes the block's rows
+ * to d_Y (row i of the block at d_Y + i * ldy), as smfv_spmm_rowblock_f64. */
+SMFV_API int smfv_plan_create_rows(smfv_plan_t *plan, int variant, int row_begin, int row_end, int n,
+                                   const int *h_row_ptr, const int *h_col_idx, int K, int flags);
 SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, void *stream);
 /* Host-only diagnostic: run the clustered tile analysis and build the tiled
  * kernel's plan, verify the invariants the kernel relies on (every row in
@@ -133,8 +157,12 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
                                const double *d_values, const double *d_X, int64_t ldx,
                                double *d_Y, int64_t ldy, void *stream);
 /* out[0] tiled (0/1), [1] tiles, [2] staged X rows per panel, [3] re-use
- * (tiled non-zeros / staged rows), [4] plan device bytes, [5] direct tiles */
-SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[6]);
+ * (tiled non-zeros / staged rows), [4] plan device bytes, [5] direct rows,
+ * [6] first row of the block, [7] re-use estimated on the sample tiles (-1:
+ * not sampled), [8] host analysis + upload time (ms), [9] values gathered
+ * by each bind (snapshot entries, pads included) */
+#define SMFV_PLAN_STATS 10
+SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS]);
 SMFV_API int smfv_plan_destroy(smfv_plan_t plan);
 
 /* HBM streaming probe for the bench (not the SpMM path): d_dst = d_src,
@@ -210,6 +238,11 @@ SMFV_API int smfv_comm_init(smfv_comm_t *comm, int nranks, int rank,
 SMFV_API int smfv_comm_destroy(smfv_comm_t comm);
 SMFV_API int smfv_comm_rank(smfv_comm_t comm);
 SMFV_API int smfv_comm_size(smfv_comm_t comm);
+/* In-place broadcast of `bytes` device bytes from root's d_buf to every
+ * rank's d_buf (ncclBroadcast over xGMI): the device-resident form of the
+ * reference's input distribution (SC/main.cpp:106-143, 9x MPI_Bcast).
+ * Collective, asynchronous on `stream`. */
+SMFV_API int smfv_comm_bcast(smfv_comm_t comm, void *d_buf, size_t bytes, int root, void *stream);
 
 /* Collective over `comm` (every rank calls it with the full A and X
  * resident on its device, as after SC/main.cpp:106-143):
@@ -255,6 +288,50 @@ SMFV_API int smfv_dist_rowpart_spmm_f64(smfv_comm_t comm, int mode, int root, in
                                         const int *d_row_ptr_local, const int *d_col_idx_local,
                                         const double *d_values_local, const double *d_X, int K,
                                         double *d_Y, void *stream);
+
+/* The exchange step as a list of operations (pure host; the schedule
+ * smfv_dist_spmm_f64 and the distributed plans execute with RCCL, exposed so
+ * it can be replayed over another transport in tests).  For rank `rank` of
+ * p: op i is kinds[i] (SMFV_EX_*) with peer, offset and count (doubles,
+ * into the exchange buffer of smfv_dist_plan); ops run in order, inside
+ * one group.  Arrays hold >= 2p entries; *nops receives the count. */
+#define SMFV_EX_ALLGATHER 1 /* ncclAllGather(buf + offset, buf + offset - rank * count, count): equal
+                              back-to-back blocks, rank r's at offset - (rank - r) * count */
+#define SMFV_EX_BCAST 2     /* ncclBroadcast(buf + offset, count, root = peer): one block of an all-gatherv */
+#define SMFV_EX_SEND 3      /* ncclSend(buf + offset, count, to peer): own block to the root */
+#define SMFV_EX_RECV 4      /* ncclRecv(buf + offset, count, from peer): a rank's block at the root */
+SMFV_API int smfv_dist_exchange_ops(int variant, int mode, int root, int m, int64_t nnz,
+                                    const int *h_row_ptr, int K, int p, int rank, int *kinds, int *peers,
+                                    int64_t *offsets, int64_t *counts, int *nops);
+
+/* ---- distributed plans: the rank-local part analysed once --------------
+ * A distributed plan holds this rank's share of a variant (RowWise row
+ * block, ColumnWise K-column window, NonZeroElement nnz range) as a
+ * single-device plan -- so the rank-local compute runs the tiled kernel
+ * where it pays, as smfv_plan_* does -- plus the exchange buffers and the
+ * exchange schedule.  h_col_idx may be NULL (no tiling).  Values contract as
+ * for smfv_plan_t (bind after a change).  execute = execute_local +
+ * exchange on the same stream; the two halves are exposed separately for
+ * timing.  mode / root as smfv_dist_spmm_f64; d_Y is m x K, row-major.
+ * Collective: every rank creates and executes its plan. */
+typedef struct smfv_dist_plan_s *smfv_dist_plan_t;
+SMFV_API int smfv_dist_plan_create(smfv_dist_plan_t *plan, smfv_comm_t comm, int variant, int mode, int root,
+                                   int m, int n, int64_t nnz, const int *h_row_ptr, const int *h_col_idx, int K,
+                                   int flags);
+/* Row-partitioned ROWWISE (A not replicated, as smfv_dist_rowpart_spmm_f64):
+ * the rank's local CSR rows of the RowWise partition of an m-row matrix. */
+SMFV_API int smfv_dist_plan_create_rowpart(smfv_dist_plan_t *plan, smfv_comm_t comm, int mode, int root, int m,
+                                           int n, const int *h_row_ptr_local, const int *h_col_idx_local, int K,
+                                           int flags);
+SMFV_API int smfv_dist_plan_bind_values(smfv_dist_plan_t plan, const double *d_values, void *stream);
+SMFV_API int smfv_dist_plan_execute(smfv_dist_plan_t plan, const int *d_row_ptr, const int *d_col_idx,
+                                    const double *d_values, const double *d_X, double *d_Y, void *stream);
+SMFV_API int smfv_dist_plan_execute_local(smfv_dist_plan_t plan, const int *d_row_ptr, const int *d_col_idx,
+                                          const double *d_values, const double *d_X, double *d_Y, void *stream);
+SMFV_API int smfv_dist_plan_exchange(smfv_dist_plan_t plan, double *d_Y, void *stream);
+/* the rank-local plan's smfv_plan_stats */
+SMFV_API int smfv_dist_plan_stats(smfv_dist_plan_t plan, double out[SMFV_PLAN_STATS]);
+SMFV_API int smfv_dist_plan_destroy(smfv_dist_plan_t plan);
 
 /* ---- vendor-library comparator (not on the product path) ---------------
  * Y = A * X by rocSPARSE's generic SpMM (CSR int32 / f64, row-major X and

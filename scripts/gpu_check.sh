@@ -10,7 +10,7 @@ TAG=${TAG:-run}
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > "$OUT/pytest_gpu_$TAG.log" 2>&1
+  timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > "$OUT/pytest_gpu_$TAG.log" 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -n 25 "$OUT/pytest_gpu_$TAG.log"
   ok $rc || exit $rc
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.log" 2>&1

@@ -11,7 +11,9 @@ import os
 from ctypes import POINTER, c_char, c_char_p, c_double, c_int, c_int64, c_size_t, c_uint64, c_void_p
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsmfv.so")
+# SMFV_LAB=1 loads the lab build (make -C csrc lab: ablation kernels and
+# environment overrides for A/B experiments); the product is libsmfv.so
+LIB_PATH = os.path.join(HERE, "libsmfv_lab.so" if os.environ.get("SMFV_LAB") == "1" else "libsmfv.so")
 
 SMFV_OK = 0
 STATUS_NAMES = {
@@ -42,12 +44,15 @@ _SIGS = {
     "smfv_partition_rows": (None, [c_int, c_int, c_int, _PI, _PI]),
     "smfv_partition_cols": (None, [c_int, c_int, c_int, _PI, _PI]),
     "smfv_partition_nnz": (None, [c_int64, c_int, c_int, _PI64, _PI64]),
+    "smfv_merge_geometry": (c_int, [c_int, c_int64, c_int, _PI64]),
     "smfv_spmm_workspace_bytes": (c_int, [c_int, c_int, c_int64, c_int, POINTER(c_size_t)]),
     "smfv_spmm_csr_f64": (c_int, [c_int, c_int, c_int, c_int64, c_void_p, c_void_p, c_void_p,
                                   c_void_p, c_int64, c_int, c_void_p, c_int64, c_void_p, c_size_t,
                                   c_void_p]),
     "smfv_plan_create": (c_int, [POINTER(c_void_p), c_int, c_int, c_int, c_int64, _PI, _PI, c_int,
                                  c_int]),
+    "smfv_plan_create_rows": (c_int, [POINTER(c_void_p), c_int, c_int, c_int, c_int, _PI, _PI, c_int,
+                                      c_int]),
     "smfv_plan_analyse": (c_int, [c_int, c_int, _PI, _PI, _PD]),
     "smfv_plan_bind_values": (c_int, [c_void_p, c_void_p, c_void_p]),
     "smfv_plan_execute": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
@@ -75,6 +80,7 @@ _SIGS = {
     "smfv_comm_destroy": (c_int, [c_void_p]),
     "smfv_comm_rank": (c_int, [c_void_p]),
     "smfv_comm_size": (c_int, [c_void_p]),
+    "smfv_comm_bcast": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     "smfv_dist_workspace_bytes": (c_int, [c_void_p, c_int, c_int, c_int64, _PI, c_int,
                                           POINTER(c_size_t)]),
     "smfv_dist_plan": (c_int, [c_int, c_int, c_int64, _PI, c_int, c_int, _PI, _PI, _PI64,
@@ -84,6 +90,19 @@ _SIGS = {
                                    c_void_p, c_size_t, c_void_p]),
     "smfv_dist_rowpart_spmm_f64": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
                                            c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "smfv_dist_exchange_ops": (c_int, [c_int, c_int, c_int, c_int, c_int64, _PI, c_int, c_int, c_int, _PI, _PI,
+                                       _PI64, _PI64, _PI]),
+    "smfv_dist_plan_create": (c_int, [POINTER(c_void_p), c_void_p, c_int, c_int, c_int, c_int, c_int, c_int64,
+                                      _PI, _PI, c_int, c_int]),
+    "smfv_dist_plan_create_rowpart": (c_int, [POINTER(c_void_p), c_void_p, c_int, c_int, c_int, c_int, _PI, _PI,
+                                              c_int, c_int]),
+    "smfv_dist_plan_bind_values": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "smfv_dist_plan_execute": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "smfv_dist_plan_execute_local": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                             c_void_p]),
+    "smfv_dist_plan_exchange": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "smfv_dist_plan_stats": (c_int, [c_void_p, _PD]),
+    "smfv_dist_plan_destroy": (c_int, [c_void_p]),
     "smfv_stream_copy": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "smfv_vendor_spmm_create": (c_int, [c_void_p, c_int, c_int, c_int, c_int64, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64, c_void_p]),

@@ -98,6 +98,14 @@ SMFV_API int smfv_comm_destroy(smfv_comm_t comm)
 SMFV_API int smfv_comm_rank(smfv_comm_t comm) { return comm ? comm->rank : -1; }
 SMFV_API int smfv_comm_size(smfv_comm_t comm) { return comm ? comm->nranks : -1; }
 
+SMFV_API int smfv_comm_bcast(smfv_comm_t comm, void *d_buf, size_t bytes, int root, void *stream)
+{
+    SMFV_REQUIRE(comm && (d_buf || bytes == 0) && root >= 0 && root < comm->nranks, "bad argument");
+    if (comm->nranks == 1 || bytes == 0) return SMFV_OK;
+    SMFV_NCCL(ncclBroadcast(d_buf, d_buf, bytes, ncclUint8, root, comm->nccl, smfv::as_stream(stream)));
+    return SMFV_OK;
+}
+
 SMFV_API int smfv_dist_plan(int variant, int m, int64_t nnz, const int *h_row_ptr, int K, int p,
                             int *first, int *last, int64_t *offset, int64_t *count)
 {
@@ -196,38 +204,90 @@ SMFV_API int smfv_dist_workspace_bytes(smfv_comm_t comm, int variant, int m, int
     return SMFV_ERR_INVALID;
 }
 
-// The one exchange step of a distributed variant: gather-to-root (Gatherv /
-// Reduce target) or all-gatherv of the ranks' blocks P.offset/P.count inside
-// xbuf; equal, back-to-back blocks go through one ncclAllGather.
+// The one exchange step of a distributed variant as data: gather-to-root
+// (Gatherv / the Reduce's target) or all-gatherv of the ranks' blocks
+// P.offset/P.count inside the exchange buffer; equal, back-to-back blocks
+// go through one all-gather.
+struct ExOp {
+    int kind, peer;
+    int64_t offset, count;
+};
+
+static std::vector<ExOp> exchange_schedule(const Plan &P, int p, int rank, bool may_be_equal, bool to_all,
+                                           int root)
+{
+    std::vector<ExOp> ops;
+    if (p <= 1) return ops;
+    bool equal = may_be_equal;
+    for (int r = 1; r < p && equal; ++r)
+        equal = P.count[r] == P.count[0] && P.offset[r] == P.offset[0] + r * P.count[0];
+    if (to_all && equal && P.count[0] > 0) {
+        ops.push_back({SMFV_EX_ALLGATHER, -1, P.offset[rank], P.count[0]});
+        return ops;
+    }
+    for (int r = 0; r < p; ++r) {
+        if (P.count[r] == 0) continue;
+        if (to_all)
+            ops.push_back({SMFV_EX_BCAST, r, P.offset[r], P.count[r]});
+        else if (rank == root && r != root)
+            ops.push_back({SMFV_EX_RECV, r, P.offset[r], P.count[r]});
+        else if (rank == r && r != root)
+            ops.push_back({SMFV_EX_SEND, root, P.offset[r], P.count[r]});
+    }
+    return ops;
+}
+
+// Runs a schedule with RCCL on `st` (one group; the all-gather alone).
+static int run_exchange(smfv_comm_t comm, const std::vector<ExOp> &ops, double *xbuf, hipStream_t st)
+{
+    if (ops.empty()) return SMFV_OK;
+    if (ops.size() == 1 && ops[0].kind == SMFV_EX_ALLGATHER) {
+        const ExOp &o = ops[0];
+        // block r lands at offset - rank * count + r * count
+        SMFV_NCCL(ncclAllGather(xbuf + o.offset, xbuf + o.offset - (int64_t)comm->rank * o.count, (size_t)o.count,
+                                ncclDouble, comm->nccl, st));
+        return SMFV_OK;
+    }
+    SMFV_NCCL(ncclGroupStart());
+    for (const ExOp &o : ops) {
+        double *blk = xbuf + o.offset;
+        const size_t cnt = (size_t)o.count;
+        switch (o.kind) {
+        case SMFV_EX_BCAST: SMFV_NCCL(ncclBroadcast(blk, blk, cnt, ncclDouble, o.peer, comm->nccl, st)); break;
+        case SMFV_EX_RECV: SMFV_NCCL(ncclRecv(blk, cnt, ncclDouble, o.peer, comm->nccl, st)); break;
+        case SMFV_EX_SEND: SMFV_NCCL(ncclSend(blk, cnt, ncclDouble, o.peer, comm->nccl, st)); break;
+        default: (void)ncclGroupEnd(); set_error("bad exchange op %d", o.kind); return SMFV_ERR_INVALID;
+        }
+    }
+    SMFV_NCCL(ncclGroupEnd());
+    return SMFV_OK;
+}
+
 static int exchange_blocks(smfv_comm_t comm, const Plan &P, bool may_be_equal, bool to_all, int root,
                            double *xbuf, hipStream_t st)
 {
-    const int p = comm->nranks, rank = comm->rank;
-    if (p > 1) {
-        bool equal = may_be_equal;
-        for (int r = 1; r < p && equal; ++r)
-            equal = P.count[r] == P.count[0] && P.offset[r] == P.offset[0] + r * P.count[0];
-        if (to_all && equal && P.count[0] > 0) {
-            SMFV_NCCL(ncclAllGather(xbuf + P.offset[rank], xbuf, (size_t)P.count[0], ncclDouble,
-                                    comm->nccl, st));
-        } else {
-            SMFV_NCCL(ncclGroupStart());
-            for (int r = 0; r < p; ++r) {
-                if (P.count[r] == 0) continue;
-                double *blk = xbuf + P.offset[r];
-                const size_t cnt = (size_t)P.count[r];
-                if (to_all) {
-                    SMFV_NCCL(ncclBroadcast(blk, blk, cnt, ncclDouble, r, comm->nccl, st));
-                } else if (rank == root && r != root) {
-                    SMFV_NCCL(ncclRecv(blk, cnt, ncclDouble, r, comm->nccl, st));
-                } else if (rank == r && r != root) {
-                    SMFV_NCCL(ncclSend(blk, cnt, ncclDouble, root, comm->nccl, st));
-                }
-            }
-            SMFV_NCCL(ncclGroupEnd());
-        }
-    }
+    return run_exchange(comm, exchange_schedule(P, comm->nranks, comm->rank, may_be_equal, to_all, root), xbuf,
+                        st);
+}
 
+SMFV_API int smfv_dist_exchange_ops(int variant, int mode, int root, int m, int64_t nnz, const int *h_row_ptr,
+                                    int K, int p, int rank, int *kinds, int *peers, int64_t *offsets,
+                                    int64_t *counts, int *nops)
+{
+    SMFV_REQUIRE(kinds && peers && offsets && counts && nops, "null output array");
+    SMFV_REQUIRE(p > 0 && rank >= 0 && rank < p && root >= 0 && root < p, "bad rank / root");
+    SMFV_REQUIRE(mode == SMFV_TO_ROOT || mode == SMFV_TO_ALL, "bad mode %d", mode);
+    Plan P;
+    int rc = make_plan(variant, m, nnz, h_row_ptr, K, p, P);
+    if (rc) return rc;
+    const auto ops = exchange_schedule(P, p, rank, variant != SMFV_NONZERO, mode == SMFV_TO_ALL, root);
+    for (size_t i = 0; i < ops.size(); ++i) {
+        kinds[i] = ops[i].kind;
+        peers[i] = ops[i].peer;
+        offsets[i] = ops[i].offset;
+        counts[i] = ops[i].count;
+    }
+    *nops = (int)ops.size();
     return SMFV_OK;
 }
 
@@ -316,6 +376,176 @@ SMFV_API int smfv_dist_rowpart_spmm_f64(smfv_comm_t comm, int mode, int root, in
     if (rc) return rc;
     // 2) the one exchange step (all-gather of equal blocks / all-gatherv / gatherv)
     return exchange_blocks(comm, P, true, mode == SMFV_TO_ALL, root, d_Y, st);
+}
+
+// ---------------------------------------------------------------------------
+// distributed plans
+// ---------------------------------------------------------------------------
+struct smfv_dist_plan_s {
+    smfv_comm_t comm = nullptr;
+    int variant = 0, mode = 0, root = 0, m = 0, n = 0, K = 0;
+    bool rowpart = false;
+    Plan P;
+    std::vector<ExOp> ops;
+    smfv_plan_t local = nullptr;  // this rank's share as a single-device plan
+    double *xbuf = nullptr;       // exchange buffer (COLUMNWISE panels / NONZERO row blocks)
+    ~smfv_dist_plan_s()
+    {
+        if (local) smfv_plan_destroy(local);
+        if (xbuf) (void)hipFree(xbuf);
+    }
+};
+
+static int dist_plan_finish(smfv_dist_plan_s *d, smfv_dist_plan_t *out)
+{
+    const int p = d->comm->nranks, rank = d->comm->rank;
+    d->ops = exchange_schedule(d->P, p, rank, d->variant != SMFV_NONZERO, d->mode == SMFV_TO_ALL, d->root);
+    if (d->variant == SMFV_COLUMNWISE || d->variant == SMFV_NONZERO) {
+        const size_t b = std::max<size_t>((size_t)d->P.total, 1) * sizeof(double);
+        hipError_t e = hipMalloc(reinterpret_cast<void **>(&d->xbuf), b);
+        if (e != hipSuccess) {
+            set_error("hipMalloc(exchange buffer): %s", hipGetErrorString(e));
+            delete d;
+            return SMFV_ERR_HIP;
+        }
+    }
+    *out = d;
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_dist_plan_create(smfv_dist_plan_t *out, smfv_comm_t comm, int variant, int mode, int root, int m,
+                                   int n, int64_t nnz, const int *h_row_ptr, const int *h_col_idx, int K, int flags)
+{
+    SMFV_REQUIRE(out && comm && h_row_ptr, "null plan / communicator / row_ptr");
+    SMFV_REQUIRE(mode == SMFV_TO_ROOT || mode == SMFV_TO_ALL, "bad mode %d", mode);
+    SMFV_REQUIRE(root >= 0 && root < comm->nranks, "bad root %d", root);
+    SMFV_REQUIRE(m >= 0 && n >= 0 && nnz >= 0 && nnz <= 0x7fffffff && K >= 0 && h_row_ptr[m] == nnz, "bad sizes");
+    SMFV_REQUIRE(variant >= SMFV_SEQUENTIAL && variant <= SMFV_NONZERO, "unknown variant %d", variant);
+    const int p = comm->nranks, rank = comm->rank;
+    auto *d = new smfv_dist_plan_s;
+    d->comm = comm;
+    d->variant = variant == SMFV_SEQUENTIAL ? SMFV_ROWWISE : variant;
+    d->mode = mode;
+    d->root = root;
+    d->m = m;
+    d->n = n;
+    d->K = K;
+    int rc = make_plan(d->variant, m, nnz, h_row_ptr, K, p, d->P);
+    if (!rc) {
+        const int f = d->P.first[rank], l = d->P.last[rank];
+        switch (d->variant) {
+        case SMFV_ROWWISE:  // rows [f, l] (SC/...RowWise.cpp:26-50)
+            rc = smfv_plan_create_rows(&d->local, SMFV_ROWWISE, f, l + 1, n, h_row_ptr, h_col_idx, K, flags);
+            break;
+        case SMFV_COLUMNWISE:  // all rows, K columns [f, l] (SC/...ColumnWise.cpp:25-48)
+            rc = smfv_plan_create(&d->local, SMFV_COLUMNWISE, m, n, nnz, h_row_ptr, h_col_idx, l - f + 1, flags);
+            break;
+        default: {  // nnz range [s, e) over rows [f, l] (SC/...NonZeroElement.cpp:24-67)
+            int64_t s, e;
+            smfv_partition_nnz(nnz, p, rank, &s, &e);
+            rc = smfv::plan_create(&d->local, SMFV_NONZERO, f, std::max(0, l - f + 1), n, s, e, nullptr, nullptr, K,
+                                   flags);
+        }
+        }
+    }
+    if (rc) {
+        delete d;
+        return rc;
+    }
+    return dist_plan_finish(d, out);
+}
+
+SMFV_API int smfv_dist_plan_create_rowpart(smfv_dist_plan_t *out, smfv_comm_t comm, int mode, int root, int m, int n,
+                                           const int *h_row_ptr_local, const int *h_col_idx_local, int K, int flags)
+{
+    SMFV_REQUIRE(out && comm && h_row_ptr_local, "null plan / communicator / row_ptr");
+    SMFV_REQUIRE(mode == SMFV_TO_ROOT || mode == SMFV_TO_ALL, "bad mode %d", mode);
+    SMFV_REQUIRE(root >= 0 && root < comm->nranks, "bad root %d", root);
+    SMFV_REQUIRE(m >= 0 && n >= 0 && K >= 0, "bad sizes");
+    auto *d = new smfv_dist_plan_s;
+    d->comm = comm;
+    d->variant = SMFV_ROWWISE;
+    d->rowpart = true;
+    d->mode = mode;
+    d->root = root;
+    d->m = m;
+    d->n = n;
+    d->K = K;
+    int rc = make_plan(SMFV_ROWWISE, m, 0, nullptr, K, comm->nranks, d->P);
+    const int mloc = d->P.last[comm->rank] - d->P.first[comm->rank] + 1;
+    if (!rc)
+        rc = smfv_plan_create(&d->local, SMFV_ROWWISE, mloc, n, h_row_ptr_local[mloc], h_row_ptr_local,
+                              h_col_idx_local, K, flags);
+    if (rc) {
+        delete d;
+        return rc;
+    }
+    return dist_plan_finish(d, out);
+}
+
+SMFV_API int smfv_dist_plan_bind_values(smfv_dist_plan_t d, const double *d_values, void *stream)
+{
+    SMFV_REQUIRE(d, "null plan");
+    return smfv_plan_bind_values(d->local, d_values, stream);
+}
+
+SMFV_API int smfv_dist_plan_execute_local(smfv_dist_plan_t d, const int *d_row_ptr, const int *d_col_idx,
+                                          const double *d_values, const double *d_X, double *d_Y, void *stream)
+{
+    SMFV_REQUIRE(d, "null plan");
+    SMFV_REQUIRE(d_Y || d->m == 0 || d->K == 0, "null Y");
+    const int rank = d->comm->rank, K = d->K;
+    const int f = d->P.first[rank], l = d->P.last[rank];
+    switch (d->variant) {
+    case SMFV_ROWWISE:  // in place: this rank's rows of Y
+        return smfv_plan_execute(d->local, d_row_ptr, d_col_idx, d_values, d_X, K, d_Y + d->P.offset[rank], K,
+                                 stream);
+    case SMFV_COLUMNWISE: {  // [m x kc] panel from the X column window
+        const int kc = l - f + 1;
+        if (kc <= 0) return SMFV_OK;
+        return smfv_plan_execute(d->local, d_row_ptr, d_col_idx, d_values, d_X + f, K, d->xbuf + d->P.offset[rank],
+                                 kc, stream);
+    }
+    default:  // compact partial rows [f, l]
+        if (l < f) return SMFV_OK;
+        return smfv_plan_execute(d->local, d_row_ptr, d_col_idx, d_values, d_X, K, d->xbuf + d->P.offset[rank], K,
+                                 stream);
+    }
+}
+
+SMFV_API int smfv_dist_plan_exchange(smfv_dist_plan_t d, double *d_Y, void *stream)
+{
+    SMFV_REQUIRE(d, "null plan");
+    hipStream_t st = smfv::as_stream(stream);
+    double *buf = d->variant == SMFV_ROWWISE ? d_Y : d->xbuf;
+    int rc = run_exchange(d->comm, d->ops, buf, st);
+    if (rc) return rc;
+    const int p = d->comm->nranks;
+    if (!(d->mode == SMFV_TO_ALL || d->comm->rank == d->root)) return SMFV_OK;
+    if (d->variant == SMFV_COLUMNWISE) return smfv_panels_to_rowmajor_f64(d->m, d->K, p, d->xbuf, d_Y, d->K, stream);
+    if (d->variant == SMFV_NONZERO)
+        return smfv_combine_row_blocks_f64(d->m, d->K, p, d->P.first.data(), d->P.last.data(), d->xbuf, d_Y, d->K,
+                                           stream);
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_dist_plan_execute(smfv_dist_plan_t d, const int *d_row_ptr, const int *d_col_idx,
+                                    const double *d_values, const double *d_X, double *d_Y, void *stream)
+{
+    int rc = smfv_dist_plan_execute_local(d, d_row_ptr, d_col_idx, d_values, d_X, d_Y, stream);
+    return rc ? rc : smfv_dist_plan_exchange(d, d_Y, stream);
+}
+
+SMFV_API int smfv_dist_plan_stats(smfv_dist_plan_t d, double out[SMFV_PLAN_STATS])
+{
+    SMFV_REQUIRE(d, "null plan");
+    return smfv_plan_stats(d->local, out);
+}
+
+SMFV_API int smfv_dist_plan_destroy(smfv_dist_plan_t d)
+{
+    delete d;
+    return SMFV_OK;
 }
 
 }  // extern "C"

@@ -44,4 +44,10 @@ struct MergeGeom {
 MergeGeom merge_geom(int nrows, int64_t nnz, int K);
 size_t merge_workspace_bytes(int nrows, int64_t nnz, int K);
 
+// smfv_plan_create / smfv_plan_create_rows with an explicit non-zero range
+// (NONZERO rank-local plans: rows [row_begin, row_begin + m) restricted to
+// the non-zeros [nnz_base, nnz_end)); h_rp / h_ci: the whole matrix or NULL.
+int plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n, int64_t nnz_base, int64_t nnz_end,
+                const int *h_rp, const int *h_ci, int K, int flags);
+
 }  // namespace smfv

@@ -34,6 +34,7 @@
 // matrix touches stay in one XCD's L2.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
@@ -440,7 +441,9 @@ template <bool NT> __device__ __forceinline__ void dma16(const void *g, unsigned
 __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 }  // namespace ws
 
-// ABL (lab A/B only, SMFV_WS_ABL): 1 staging only (no compute), 2 compute
+// ABL (lab A/B only: instantiated in the lab build, libsmfv_lab.so with
+// -DSMFV_LAB, selected there by SMFV_WS_ABL; libsmfv.so has ABL = 0 only):
+// 1 staging only (no compute), 2 compute
 // only (every unit recomputes the first staged tile), 3 as 2 without Y stores,
 // 4 as 2 without the per-unit barriers (waves run their units unsynchronised),
 // 5 staging and compute both running, decoupled (no barriers; compute reads
@@ -633,10 +636,13 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
 }
 
 // Rows the ws plan could not tile (over a cap alone): one 8-lane team per
-// row, X gathered straight from HBM, CSR order (bit-identical).
+// row, X gathered straight from HBM, CSR order (bit-identical).  `rows` are
+// block-local (Y row), row_begin + row indexes the CSR; the values come from
+// the plan's bound snapshot (tv + doff[team], CSR order), like the tiles'.
 __global__ __launch_bounds__(256) void k_rows_list(int nrows, const int *__restrict__ rows,
+                                                   const int64_t *__restrict__ doff, int row_begin,
                                                    const int *__restrict__ rp, const int *__restrict__ ci,
-                                                   const double *__restrict__ va,
+                                                   const double *__restrict__ tv,
                                                    const double *__restrict__ X, int64_t ldx,
                                                    double *__restrict__ Y, int64_t ldy)
 {
@@ -645,10 +651,12 @@ __global__ __launch_bounds__(256) void k_rows_list(int nrows, const int *__restr
     const int tl = threadIdx.x & 7, par = (threadIdx.x >> 3) & 1;
     const int cp = blockIdx.y * TILE_KP;
     const int row = rows[team];
+    const int j0 = rp[row_begin + row];
+    const double *vrow = tv + doff[team] - j0;
     double2 acc0 = make_double2(0.0, 0.0), acc1 = make_double2(0.0, 0.0);
-    for (int jj = rp[row]; jj < rp[row + 1]; ++jj) {
+    for (int jj = j0; jj < rp[row_begin + row + 1]; ++jj) {
         const double *px = X + (int64_t)ci[jj] * ldx + cp + 2 * tl;
-        const double v = va[jj];
+        const double v = vrow[jj];
         acc0 = VecT<2>::madd(acc0, v, *reinterpret_cast<const double2 *>(px + 16 * par));
         acc1 = VecT<2>::madd(acc1, v, *reinterpret_cast<const double2 *>(px + 16 * (par ^ 1)));
     }
@@ -1017,19 +1025,22 @@ static int pick_team(int K, int vec)
     }
 
 // Row-kernel configuration (TEAM lanes per row, H column groups per lane,
-// U gathers in flight per team) by K; SMFV_ROW_CFG="TEAM,H,U" overrides it
-// for A/B measurement (only configurations instantiated below exist).
+// U gathers in flight per team) by K; in the lab build (-DSMFV_LAB)
+// SMFV_ROW_CFG="TEAM,H,U" overrides it for A/B measurement (only
+// configurations instantiated below exist).
 struct RowCfg {
     int team, h, u;
 };
 
 static RowCfg row_cfg_for(int K)
 {
+#ifdef SMFV_LAB
     static const char *env = std::getenv("SMFV_ROW_CFG");
     if (env) {
         RowCfg c{0, 0, 0};
         if (std::sscanf(env, "%d,%d,%d", &c.team, &c.h, &c.u) == 3) return c;
     }
+#endif
     const int pairs = K / 2;  // double2 columns
     if (pairs >= 64) return {16, 4, 4};
     if (pairs >= 16) return {8, 2, 8};
@@ -1146,10 +1157,14 @@ static int launch_merge(int row_first, int nrows, int64_t s, int64_t e, const in
     const int tpb = 256 / team;
     const int64_t nblk = (g.nteams + tpb - 1) / tpb;
     SMFV_REQUIRE(nblk <= 0x7fffffff, "too many merge teams for one launch");
-    static const bool flat = [] {  // A/B: SMFV_MERGE_FLAT=0 keeps the per-row k_merge
+#ifdef SMFV_LAB
+    static const bool flat = [] {  // lab A/B: SMFV_MERGE_FLAT=0 keeps the per-row k_merge
         const char *ev = std::getenv("SMFV_MERGE_FLAT");
         return !ev || std::atoi(ev) != 0;
     }();
+#else
+    constexpr bool flat = true;
+#endif
     if (flat && vec == 2 && K % 32 == 0) {
         const int64_t fblk_ = (g.nteams + 15) / 16;
         hipLaunchKernelGGL((k_merge_flat<16>), dim3((unsigned)fblk_), dim3(256), 0, st, row_first, nrows, s, e, rp,
@@ -1211,6 +1226,16 @@ SMFV_API void smfv_partition_nnz(int64_t nnz, int p, int r, int64_t *start, int6
     }
 }
 
+SMFV_API int smfv_merge_geometry(int nrows, int64_t nnz, int K, int64_t out[3])
+{
+    SMFV_REQUIRE(out && nrows >= 0 && nnz >= 0 && K >= 0, "bad argument");
+    const MergeGeom g = merge_geom(nrows, nnz, K);
+    out[0] = g.items;
+    out[1] = g.ipt;
+    out[2] = g.nteams;
+    return SMFV_OK;
+}
+
 SMFV_API int smfv_spmm_workspace_bytes(int variant, int m, int64_t nnz, int K, size_t *bytes)
 {
     SMFV_REQUIRE(bytes != nullptr, "bytes is NULL");
@@ -1238,18 +1263,16 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz, const int
     case SMFV_SEQUENTIAL:
     case SMFV_ROWWISE:
         return launch_rows(0, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, n, K, d_Y, ldy, st);
-    case SMFV_COLUMNWISE: {
-        // column panels of 8 doubles (64 B per row segment), one launch per
-        // panel group; same per-(row, column) summation as the reference.
-        const int kc = 8;
-        for (int c0 = 0; c0 < K; c0 += kc) {
-            const int w = std::min(kc, K - c0);
-            int rc = launch_rows(0, m, d_row_ptr, d_col_idx, d_values, d_X + c0, ldx, n, w, d_Y + c0,
-                                 ldy, st);
-            if (rc) return rc;
-        }
-        return SMFV_OK;
-    }
+    case SMFV_COLUMNWISE:
+        // The reference's ColumnWise splits the K columns into per-rank
+        // panels (SC/...ColumnWise.cpp:25-48); each panel's entries are the
+        // same per-row, CSR-ordered sums.  On one device every panel of a row
+        // is computed by the row's team in ONE pass over its CSR segment
+        // (the panels are the team's column groups / the tiled kernel's
+        // 32-column units), so A is streamed once, not once per panel.
+        // The per-rank panel of the distributed variant is
+        // smfv_spmm_colpanel_f64 / a column-window plan (smfv_dist.cpp).
+        return launch_rows(0, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, n, K, d_Y, ldy, st);
     case SMFV_NONZERO:
         return launch_merge(0, m, 0, nnz, d_row_ptr, d_col_idx, d_values, d_X, ldx, K, d_Y, ldy,
                             d_workspace, workspace_bytes, st);
@@ -1261,28 +1284,40 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz, const int
 }  // extern "C"
 
 constexpr double SMFV_TILE_MIN_REUSE = 3.0;
-constexpr int SMFV_TILE_SAMPLE_ROWS = 16384;  // rows analysed first to estimate re-use
+// Tiles grown first (from the first rows, in the FULL pattern) to estimate
+// re-use before the whole analysis is run; growing them in the full pattern
+// makes the estimate independent of the row numbering (a sample of the first
+// rows' own sub-pattern misjudges a permuted matrix).
+constexpr int SMFV_TILE_SAMPLE_TILES = 512;
+constexpr int SMFV_TILE_SAMPLE_MIN_ROWS = 16384;  // below this the full analysis runs directly
 
 struct smfv_plan_s {
     int variant = 0, m = 0, n = 0, K = 0;
+    int row_begin = 0;                     // first CSR row of the plan's row block
+    int64_t nnz_base = 0, nnz_end = 0;     // the block's CSR range [row_ptr[row_begin], row_ptr[row_end])
     bool fma = false;  // SMFV_PLAN_FMA: fused multiply-add in the tiled kernel (not bit-identical)
-    int64_t nnz = 0;
+    int64_t nnz = 0;                       // non-zeros of the block
     bool tiled = false;
     int ntiles = 0, ndirect = 0;
     int64_t union_rows = 0, tiled_nnz = 0, padded_nnz = 0;
-    double reuse = 0.0;
-    int *tsrc = nullptr;                   // entry -> CSR index of its value (-1: pad)
-    double *tvals = nullptr;               // tile-ordered values (pads -0.0)
-    const double *bound_values = nullptr;  // d_values the tile-ordered copy came from
+    int64_t snapshot = 0;                  // values gathered by bind (tile entries + slack + direct rows)
+    double reuse = 0.0, est_reuse = -1.0, analysis_ms = 0.0;
+    int *tsrc = nullptr;                   // snapshot entry -> CSR index of its value (-1: pad)
+    double *tvals = nullptr;               // the bound values snapshot (tile order, pads -0.0, then direct rows)
+    const double *bound_values = nullptr;  // d_values the snapshot came from
     int *ws_grec = nullptr, *ws_lrec = nullptr, *direct_rows = nullptr;
+    int64_t *direct_off = nullptr;         // per direct row: its first value in tvals
     uint16_t *ws_loff = nullptr;
     void *ws = nullptr;
     size_t ws_bytes = 0, dev_bytes = 0;
+    hipEvent_t bind_ev = nullptr;          // recorded after the snapshot gather
+    hipStream_t bind_stream = nullptr;
     ~smfv_plan_s()
     {
         for (void *q : {(void *)tsrc, (void *)tvals, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
-                        (void *)ws_loff, ws})
+                        (void *)direct_off, (void *)ws_loff, ws})
             if (q) (void)hipFree(q);
+        if (bind_ev) (void)hipEventDestroy(bind_ev);
     }
 };
 
@@ -1295,75 +1330,92 @@ template <class T> int upload(T **dst, const std::vector<T> &src, size_t &acc)
     acc += b;
     return SMFV_OK;
 }
+
 }  // namespace
 
-extern "C" {
-
-SMFV_API int smfv_plan_create(smfv_plan_t *out, int variant, int m, int n, int64_t nnz,
-                              const int *h_row_ptr, const int *h_col_idx, int K, int flags)
+// Plan of rows [row_begin, row_begin + m) of a CSR matrix: h_rp / h_ci are the
+// host arrays of the WHOLE matrix (or NULL: no tiling); the analysis runs on
+// the block's own view (local row ids, its slice of col_idx), the snapshot
+// indexes the whole matrix's values.  NONZERO plans cover the non-zeros
+// [nnz_base, nnz_end) of the block's rows (a rank's nnz range).
+int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n, int64_t nnz_base, int64_t nnz_end,
+                const int *h_rp, const int *h_ci, int K, int flags)
 {
-    SMFV_REQUIRE(out, "null plan pointer");
-    SMFV_REQUIRE(variant >= SMFV_SEQUENTIAL && variant <= SMFV_NONZERO, "unknown variant %d", variant);
-    SMFV_REQUIRE(m >= 0 && n >= 0 && nnz >= 0 && nnz <= 0x7fffffff && K >= 0, "bad sizes");
-    SMFV_REQUIRE(h_row_ptr == nullptr || h_row_ptr[m] == nnz, "row_ptr[m] != nnz");
+    const auto t_start = std::chrono::steady_clock::now();
     auto *p = new smfv_plan_s;
     p->fma = (flags & SMFV_PLAN_FMA) != 0;
     p->variant = variant;
+    p->row_begin = row_begin;
     p->m = m;
     p->n = n;
     p->K = K;
-    p->nnz = nnz;
+    p->nnz_base = nnz_base;
+    p->nnz_end = nnz_end;
+    p->nnz = nnz_end - nnz_base;
     int rc = SMFV_OK;
+    auto fail_hip = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && !rc) {
+            set_error("%s: %s", what, hipGetErrorString(e));
+            rc = SMFV_ERR_HIP;
+        }
+    };
+    fail_hip(hipEventCreateWithFlags(&p->bind_ev, hipEventDisableTiming), "hipEventCreate");
     if (variant == SMFV_NONZERO) {
-        p->ws_bytes = merge_workspace_bytes(m, nnz, K);
+        p->ws_bytes = merge_workspace_bytes(m, p->nnz, K);
         if (p->ws_bytes) {
-            hipError_t e = hipMalloc(&p->ws, p->ws_bytes);
-            if (e != hipSuccess) {
-                set_error("hipMalloc(workspace): %s", hipGetErrorString(e));
-                rc = SMFV_ERR_HIP;
-            }
+            fail_hip(hipMalloc(&p->ws, p->ws_bytes), "hipMalloc(workspace)");
             p->dev_bytes += p->ws_bytes;
         }
-    } else if (h_row_ptr && h_col_idx && m > 0 && K > 0 && K % TILE_KP == 0 &&
-               !(flags & SMFV_PLAN_NO_TILES)) {
+    } else if (!rc && h_rp && h_ci && m > 0 && K > 0 && K % TILE_KP == 0 && !(flags & SMFV_PLAN_NO_TILES)) {
+        std::vector<int> rpl((size_t)m + 1);
+        for (int i = 0; i <= m; ++i) rpl[i] = (int)(h_rp[row_begin + i] - nnz_base);
+        const int *cil = h_ci + nnz_base;
         bool go = true;
-        if (!(flags & SMFV_PLAN_FORCE_TILES) && m > SMFV_TILE_SAMPLE_ROWS) {
-            // estimate re-use on a leading block of rows first (the analysis
-            // of the full pattern costs O(nnz * candidates))
-            const int ms = SMFV_TILE_SAMPLE_ROWS;
-            std::vector<int> rps(h_row_ptr, h_row_ptr + ms + 1);
+        if (!(flags & SMFV_PLAN_FORCE_TILES) && m > SMFV_TILE_SAMPLE_MIN_ROWS) {
+            // estimate re-use on the first tiles before the full analysis
+            // (which costs O(nnz * candidates))
+            TileCaps caps;
+            caps.max_tiles = SMFV_TILE_SAMPLE_TILES;
             TileAnalysis T;
-            analyse_tiles(ms, n, rps.data(), h_col_idx, T);
-            const double est = T.union_rows ? (double)T.tiled_nnz / (double)T.union_rows : 0.0;
-            go = est >= SMFV_TILE_MIN_REUSE;
+            analyse_tiles(m, n, rpl.data(), cil, T, caps);
+            p->est_reuse = T.union_rows ? (double)T.tiled_nnz / (double)T.union_rows : 0.0;
+            go = p->est_reuse >= SMFV_TILE_MIN_REUSE;
         }
         if (go) {
             WsPlan W;
             std::string err;
-            if (!build_ws_plan(m, n, h_row_ptr, h_col_idx, W, &err)) {
+            if (!build_ws_plan(m, n, rpl.data(), cil, W, &err)) {
                 set_error("%s", err.c_str());
                 rc = SMFV_ERR_INVALID;
             } else {
                 p->ntiles = W.ntiles;
                 p->union_rows = W.union_rows;
                 p->tiled_nnz = W.tiled_nnz;
-                p->padded_nnz = (int64_t)W.tsrc.size();
+                p->padded_nnz = W.entries;
                 p->ndirect = (int)W.direct.size();
                 p->reuse = W.union_rows ? (double)W.tiled_nnz / (double)W.union_rows : 0.0;
                 if (p->reuse >= SMFV_TILE_MIN_REUSE || (flags & SMFV_PLAN_FORCE_TILES)) {
                     p->tiled = true;
+                    // snapshot sources: tile entries (+ DMA slack), then each direct row's values in CSR order
+                    std::vector<int> &ts = W.tsrc;
+                    for (int &s : ts)
+                        if (s >= 0) s += (int)nnz_base;
+                    std::vector<int64_t> doff;
+                    doff.reserve(W.direct.size());
+                    for (int r : W.direct) {
+                        doff.push_back((int64_t)ts.size());
+                        for (int j = rpl[r]; j < rpl[r + 1]; ++j) ts.push_back((int)(nnz_base + j));
+                    }
+                    p->snapshot = (int64_t)ts.size();
                     if (!rc) rc = upload(&p->ws_grec, W.grec, p->dev_bytes);
                     if (!rc) rc = upload(&p->ws_lrec, W.lrec, p->dev_bytes);
                     if (!rc) rc = upload(&p->ws_loff, W.loff, p->dev_bytes);
-                    if (!rc) rc = upload(&p->tsrc, W.tsrc, p->dev_bytes);
+                    if (!rc) rc = upload(&p->tsrc, ts, p->dev_bytes);
                     if (!rc) rc = upload(&p->direct_rows, W.direct, p->dev_bytes);
+                    if (!rc) rc = upload(&p->direct_off, doff, p->dev_bytes);
                     if (!rc) {
-                        const size_t b = std::max<size_t>((size_t)p->padded_nnz, 1) * sizeof(double);
-                        hipError_t e = hipMalloc(reinterpret_cast<void **>(&p->tvals), b);
-                        if (e != hipSuccess) {
-                            set_error("hipMalloc(tvals): %s", hipGetErrorString(e));
-                            rc = SMFV_ERR_HIP;
-                        }
+                        const size_t b = std::max<size_t>((size_t)p->snapshot, 1) * sizeof(double);
+                        fail_hip(hipMalloc(reinterpret_cast<void **>(&p->tvals), b), "hipMalloc(tvals)");
                         p->dev_bytes += b;
                     }
                 }
@@ -1374,9 +1426,35 @@ SMFV_API int smfv_plan_create(smfv_plan_t *out, int variant, int m, int n, int64
         delete p;
         return rc;
     }
+    p->analysis_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     *out = p;
     return SMFV_OK;
 }
+
+extern "C" {
+
+SMFV_API int smfv_plan_create(smfv_plan_t *out, int variant, int m, int n, int64_t nnz,
+                              const int *h_row_ptr, const int *h_col_idx, int K, int flags)
+{
+    SMFV_REQUIRE(out, "null plan pointer");
+    SMFV_REQUIRE(variant >= SMFV_SEQUENTIAL && variant <= SMFV_NONZERO, "unknown variant %d", variant);
+    SMFV_REQUIRE(m >= 0 && n >= 0 && nnz >= 0 && nnz <= 0x7fffffff && K >= 0, "bad sizes");
+    SMFV_REQUIRE(h_row_ptr == nullptr || (h_row_ptr[0] == 0 && h_row_ptr[m] == nnz), "row_ptr[0] != 0 or row_ptr[m] != nnz");
+    return plan_create(out, variant, 0, m, n, 0, nnz, h_row_ptr, h_row_ptr ? h_col_idx : nullptr, K, flags);
+}
+
+SMFV_API int smfv_plan_create_rows(smfv_plan_t *out, int variant, int row_begin, int row_end, int n,
+                                   const int *h_row_ptr, const int *h_col_idx, int K, int flags)
+{
+    SMFV_REQUIRE(out && h_row_ptr, "null plan pointer / row_ptr");
+    SMFV_REQUIRE(variant >= SMFV_SEQUENTIAL && variant <= SMFV_NONZERO, "unknown variant %d", variant);
+    SMFV_REQUIRE(row_begin >= 0 && row_end >= row_begin && n >= 0 && K >= 0, "bad row block [%d, %d)", row_begin,
+                 row_end);
+    const int64_t s = h_row_ptr[row_begin], e = h_row_ptr[row_end];
+    SMFV_REQUIRE(0 <= s && s <= e && e <= 0x7fffffff, "bad row_ptr range [%lld, %lld)", (long long)s, (long long)e);
+    return plan_create(out, variant, row_begin, row_end - row_begin, n, s, e, h_row_ptr, h_col_idx, K, flags);
+}
+
 
 SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_col_idx,
                                double out[6])
@@ -1441,15 +1519,20 @@ SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, voi
     SMFV_REQUIRE(plan, "null plan");
     if (!plan->tiled) return SMFV_OK;
     SMFV_REQUIRE(d_values || plan->nnz == 0, "null values");
-    const int64_t cnt = plan->padded_nnz;
+    hipStream_t st = as_stream(stream);
+    const int64_t cnt = plan->snapshot;
     if (cnt > 0) {
-        hipLaunchKernelGGL(k_gather_vals, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0,
-                           as_stream(stream), cnt, plan->tsrc, d_values, plan->tvals, -0.0);
+        hipLaunchKernelGGL(k_gather_vals, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, cnt, plan->tsrc,
+                           d_values, plan->tvals, -0.0);
         SMFV_LAUNCHED();
     }
+    // executes on another stream wait for this gather (smfv_plan_execute)
+    SMFV_HIP(hipEventRecord(plan->bind_ev, st));
+    plan->bind_stream = st;
     plan->bound_values = d_values;
     return SMFV_OK;
 }
+
 
 SMFV_API int smfv_stream_copy(void *d_dst, const void *d_src, size_t bytes, void *stream)
 {
@@ -1469,7 +1552,7 @@ SMFV_API int smfv_plan_destroy(smfv_plan_t plan)
     return SMFV_OK;
 }
 
-SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[6])
+SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS])
 {
     SMFV_REQUIRE(plan && out, "null argument");
     out[0] = plan->tiled ? 1.0 : 0.0;
@@ -1478,6 +1561,10 @@ SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[6])
     out[3] = plan->reuse;
     out[4] = (double)plan->dev_bytes;
     out[5] = plan->ndirect;
+    out[6] = plan->row_begin;
+    out[7] = plan->est_reuse;
+    out[8] = plan->analysis_ms;
+    out[9] = (double)plan->snapshot;
     return SMFV_OK;
 }
 
@@ -1489,13 +1576,31 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     const int m = plan->m, K = plan->K;
     SMFV_REQUIRE(ldx >= K && ldy >= K, "leading dimension smaller than K");
     if (m == 0 || K == 0) return SMFV_OK;
-    if (!plan->tiled || pick_vec(d_X, ldx, d_Y, ldy, K) != 2)
-        return smfv_spmm_csr_f64(plan->variant, m, plan->n, plan->nnz, d_row_ptr, d_col_idx, d_values,
-                                 d_X, ldx, K, d_Y, ldy, plan->ws, plan->ws_bytes, stream);
-    SMFV_REQUIRE(d_row_ptr && d_X && d_Y && d_values, "null argument");
+    SMFV_REQUIRE(d_row_ptr && d_Y, "null row_ptr / Y");
+    SMFV_REQUIRE(plan->nnz == 0 || (d_col_idx && d_values && d_X), "null col_idx / values / X");
+    hipStream_t st = as_stream(stream);
+    if (!plan->tiled || pick_vec(d_X, ldx, d_Y, ldy, K) != 2) {
+        // untiled: the row / merge kernels on the live values
+        if (plan->variant == SMFV_NONZERO)
+            return launch_merge(plan->row_begin, m, plan->nnz_base, plan->nnz_end, d_row_ptr, d_col_idx, d_values,
+                                d_X, ldx, K, d_Y, ldy, plan->ws, plan->ws_bytes, st);
+        return launch_rows(plan->row_begin, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, plan->n, K, d_Y, ldy, st);
+    }
     if (d_values != plan->bound_values) {
         set_error("tiled plan: values not bound (call smfv_plan_bind_values with these d_values)");
         return SMFV_ERR_INVALID;
+    }
+    if (st != plan->bind_stream) {
+        // the snapshot was gathered on another stream: order this launch after it
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        SMFV_HIP(hipStreamIsCapturing(st, &cs));
+        if (cs == hipStreamCaptureStatusNone) {
+            SMFV_HIP(hipStreamWaitEvent(st, plan->bind_ev, 0));
+        } else if (hipEventQuery(plan->bind_ev) != hipSuccess) {
+            set_error("tiled plan: the values snapshot (bound on another stream) is still in flight while "
+                      "capturing; synchronize the bind stream before capture");
+            return SMFV_ERR_INVALID;
+        }
     }
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess) {
@@ -1505,6 +1610,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     if (plan->ntiles > 0) {
         // one persistent block per CU; a multiple of 8 (>= 8) so every XCD's tile range has blocks
         const int blocks = std::max(8, (std::min(plan->ntiles, ncu) + 7) & ~7);
+#ifdef SMFV_LAB
         static const int abl = [] {  // lab-only ablations (k_rows_ws ABL modes)
             const char *e = std::getenv("SMFV_WS_ABL");
             return e ? std::atoi(e) : 0;
@@ -1512,19 +1618,22 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         auto kern = plan->fma ? (abl == 2 ? k_rows_ws<2, true> : k_rows_ws<0, true>)
                   : abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3>
                   : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : abl == 6 ? k_rows_ws<6> : k_rows_ws<0>;
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, as_stream(stream), plan->ntiles, K / TILE_KP,
+#else
+        auto kern = plan->fma ? k_rows_ws<0, true> : k_rows_ws<0>;
+#endif
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, st, plan->ntiles, K / TILE_KP,
                            plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();
     }
     if (plan->ndirect > 0) {
-        SMFV_REQUIRE(d_col_idx, "null col_idx");
         hipLaunchKernelGGL(k_rows_list, dim3((unsigned)((plan->ndirect + 31) / 32), (unsigned)(K / TILE_KP)),
-                           dim3(256), 0, as_stream(stream), plan->ndirect, plan->direct_rows, d_row_ptr, d_col_idx,
-                           d_values, d_X, ldx, d_Y, ldy);
+                           dim3(256), 0, st, plan->ndirect, plan->direct_rows, plan->direct_off, plan->row_begin,
+                           d_row_ptr, d_col_idx, plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();
     }
     return SMFV_OK;
 }
+
 
 SMFV_API int smfv_spmm_rowblock_f64(int row_begin, int row_end, int n, const int *d_row_ptr,
                                     const int *d_col_idx, const double *d_values,

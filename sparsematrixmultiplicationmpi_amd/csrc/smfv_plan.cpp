@@ -37,6 +37,7 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A, 
     int next_free = 0;
     for (int seed = 0; seed < m; ++seed) {
         if (assigned[seed]) continue;
+        if (caps.max_tiles > 0 && tile >= caps.max_tiles) break;
         next_free = seed + 1;
         int ucount = 0;
         int64_t tnnz = 0, tpad = 0;  // real and row-padded non-zeros

@@ -79,6 +79,7 @@ struct TileCaps {
     int ncap = WS_NCAP - 192;      // padded non-zeros (room for the quads' interleave padding)
     int maxrows = WS_ROWS;         // rows
     int pad = 8;                   // row segments padded to a multiple of this (power of 2)
+    int max_tiles = 0;             // > 0: stop after this many tiles (re-use estimate on a sample)
 };
 void analyse_tiles(int m, int n, const int *row_ptr, const int *col_idx, TileAnalysis &out,
                    const TileCaps &caps = TileCaps());

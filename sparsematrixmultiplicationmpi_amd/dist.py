@@ -86,6 +86,29 @@ class Communicator:
             pass
 
 
+EX_ALLGATHER, EX_BCAST, EX_SEND, EX_RECV = 1, 2, 3, 4  # SMFV_EX_*
+
+
+def exchange_ops(variant: int, mode: int, root: int, m: int, nnz: int, row_ptr: np.ndarray | None, K: int,
+                 p: int, rank: int) -> list[tuple[int, int, int, int]]:
+    """Native smfv_dist_exchange_ops: the exchange step of `rank` as a list
+    of (kind, peer, offset, count) -- the schedule the RCCL path runs."""
+    cap = 2 * p + 2
+    kinds = np.zeros(cap, np.int32)
+    peers = np.zeros(cap, np.int32)
+    offs = np.zeros(cap, np.int64)
+    cnts = np.zeros(cap, np.int64)
+    n = c_int(0)
+    rp = None
+    if row_ptr is not None:
+        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
+        rp = row_ptr.ctypes.data_as(POINTER(c_int))
+    call("smfv_dist_exchange_ops", int(variant), int(mode), int(root), m, nnz, rp, K, p, rank,
+         kinds.ctypes.data_as(POINTER(c_int)), peers.ctypes.data_as(POINTER(c_int)),
+         offs.ctypes.data_as(POINTER(c_int64)), cnts.ctypes.data_as(POINTER(c_int64)), byref(n))
+    return [(int(kinds[i]), int(peers[i]), int(offs[i]), int(cnts[i])) for i in range(n.value)]
+
+
 def dist_workspace_bytes(comm: Communicator, variant: int, A: DeviceCSR, K: int) -> int:
     b = c_size_t(0)
     call("smfv_dist_workspace_bytes", comm.handle, int(variant), A.m, A.nnz,
@@ -94,28 +117,74 @@ def dist_workspace_bytes(comm: Communicator, variant: int, A: DeviceCSR, K: int)
 
 
 class DistPlan:
-    """Pre-sized distributed execution (workspace allocated once)."""
+    """A distributed variant analysed once (smfv_dist_plan_create): this
+    rank's share (RowWise row block, ColumnWise K-column window,
+    NonZeroElement nnz range) as a single-device plan -- the tiled kernel
+    where it pays -- plus the exchange buffers and schedule.
+
+    rowpart=True: A holds only this rank's rows of the RowWise partition of
+    an m-row matrix (smfv_dist_plan_create_rowpart; `m` required)."""
 
     def __init__(self, comm: Communicator, variant: int, A: DeviceCSR, K: int, to_all: bool,
-                 root: int = 0):
+                 root: int = 0, tiles: str = "auto", rowpart: bool = False, m: int | None = None,
+                 stream=None):
         self.comm, self.variant, self.A, self.K = comm, Variant(variant), A, K
         self.mode = TO_ALL if to_all else TO_ROOT
         self.root = root
-        nb = dist_workspace_bytes(comm, variant, A, K)
-        self.ws_bytes = nb
-        self.workspace = torch.empty(max(nb, 1), dtype=torch.uint8, device=A.device)
+        self.m = A.m if not rowpart else int(m)
+        flags = {"auto": 0, "off": 1, "force": 2}[tiles]
+        ip = POINTER(c_int)
+        self._h = c_void_p()
+        if rowpart:
+            call("smfv_dist_plan_create_rowpart", byref(self._h), comm.handle, self.mode, root, self.m, A.n,
+                 A.h_row_ptr.ctypes.data_as(ip), A.h_col_idx.ctypes.data_as(ip), K, flags)
+        else:
+            call("smfv_dist_plan_create", byref(self._h), comm.handle, int(variant), self.mode, root, A.m, A.n,
+                 A.nnz, A.h_row_ptr.ctypes.data_as(ip), A.h_col_idx.ctypes.data_as(ip), K, flags)
+        self.bind_values(stream)
+
+    def bind_values(self, stream=None) -> None:
+        call("smfv_dist_plan_bind_values", self._h, self.A.values.data_ptr(), stream_handle(stream))
+
+    def _check(self, X: torch.Tensor, Y: torch.Tensor) -> None:
+        if X.shape != (self.A.n, self.K) or not X.is_contiguous() or X.dtype != torch.float64:
+            raise ValueError("X must be a contiguous float64 (n, K) device tensor")
+        if Y.shape != (self.m, self.K) or not Y.is_contiguous() or Y.dtype != torch.float64:
+            raise ValueError("Y must be a contiguous float64 (m, K) device tensor")
 
     def run(self, X: torch.Tensor, Y: torch.Tensor, stream=None) -> torch.Tensor:
-        A = self.A
-        if X.shape != (A.n, self.K) or not X.is_contiguous() or X.dtype != torch.float64:
-            raise ValueError("X must be a contiguous float64 (n, K) device tensor")
-        if Y.shape != (A.m, self.K) or not Y.is_contiguous() or Y.dtype != torch.float64:
-            raise ValueError("Y must be a contiguous float64 (m, K) device tensor")
-        rp, ci, va = A.ptrs()
-        call("smfv_dist_spmm_f64", self.comm.handle, int(self.variant), self.mode, self.root, A.m,
-             A.n, A.nnz, A.h_row_ptr.ctypes.data_as(POINTER(c_int)), rp, ci, va, X.data_ptr(),
-             self.K, Y.data_ptr(), self.workspace.data_ptr(), self.ws_bytes, stream_handle(stream))
+        self._check(X, Y)
+        rp, ci, va = self.A.ptrs()
+        call("smfv_dist_plan_execute", self._h, rp, ci, va, X.data_ptr(), Y.data_ptr(), stream_handle(stream))
         return Y
+
+    def run_local(self, X: torch.Tensor, Y: torch.Tensor, stream=None) -> torch.Tensor:
+        """The rank-local compute alone (no exchange)."""
+        self._check(X, Y)
+        rp, ci, va = self.A.ptrs()
+        call("smfv_dist_plan_execute_local", self._h, rp, ci, va, X.data_ptr(), Y.data_ptr(),
+             stream_handle(stream))
+        return Y
+
+    def exchange(self, Y: torch.Tensor, stream=None) -> torch.Tensor:
+        """The exchange step alone (after run_local)."""
+        call("smfv_dist_plan_exchange", self._h, Y.data_ptr(), stream_handle(stream))
+        return Y
+
+    def stats(self) -> dict:
+        from .engine import PLAN_STATS
+        out = (ctypes.c_double * PLAN_STATS)()
+        call("smfv_dist_plan_stats", self._h, out)
+        return {"tiled": bool(out[0]), "tiles": int(out[1]), "reuse": float(out[3]),
+                "row_begin": int(out[6]), "analysis_ms": float(out[8])}
+
+    def __del__(self):
+        try:
+            if self._h:
+                call("smfv_dist_plan_destroy", self._h)
+                self._h = c_void_p()
+        except Exception:
+            pass
 
 
 def dist_spmm(comm: Communicator, variant: int, A: DeviceCSR, X: torch.Tensor, to_all: bool = False,
@@ -125,7 +194,22 @@ def dist_spmm(comm: Communicator, variant: int, A: DeviceCSR, X: torch.Tensor, t
     K = X.shape[1]
     if Y is None:
         Y = torch.zeros((A.m, K), dtype=torch.float64, device=A.device)
-    return DistPlan(comm, variant, A, K, to_all, root).run(X, Y, stream)
+    return DistPlan(comm, variant, A, K, to_all, root, stream=stream).run(X, Y, stream)
+
+
+def dist_spmm_oneshot(comm: Communicator, variant: int, A: DeviceCSR, X: torch.Tensor, to_all: bool = False,
+                      root: int = 0, Y: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """The same through smfv_dist_spmm_f64 (no plan: workspace per call, row kernel)."""
+    K = X.shape[1]
+    if Y is None:
+        Y = torch.zeros((A.m, K), dtype=torch.float64, device=A.device)
+    nb = dist_workspace_bytes(comm, variant, A, K)
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=A.device)
+    rp, ci, va = A.ptrs()
+    call("smfv_dist_spmm_f64", comm.handle, int(variant), TO_ALL if to_all else TO_ROOT, root, A.m,
+         A.n, A.nnz, A.h_row_ptr.ctypes.data_as(POINTER(c_int)), rp, ci, va, X.data_ptr(),
+         K, Y.data_ptr(), ws.data_ptr(), nb, stream_handle(stream))
+    return Y
 
 
 def dist_rowpart_spmm(comm: Communicator, m: int, A_local: DeviceCSR, X: torch.Tensor, Y: torch.Tensor,

@@ -49,7 +49,12 @@ def stream_handle(stream: torch.cuda.Stream | None = None) -> int:
 
 class DeviceCSR:
     """A CSR matrix resident in HBM (int32 row_ptr / col_idx, f64 values)
-    plus the host copy of row_ptr the nnz partitioning needs."""
+    plus the host copy of the pattern the plans analyse.
+
+    spmm() keeps one plan per (variant, K) on the matrix (analysed once).  A
+    tiled plan computes with a snapshot of the values taken when it was bound
+    (include/smfv.h, values contract): after changing `values` in place call
+    values_changed(), which re-binds every cached plan."""
 
     def __init__(self, A: SparseMatrix, device: torch.device | None = None):
         device = device or _require_device()
@@ -61,6 +66,7 @@ class DeviceCSR:
         self.col_idx = torch.from_numpy(self.h_col_idx).to(device)
         self.values = torch.from_numpy(np.ascontiguousarray(A.values, dtype=np.float64)).to(device)
         self.device = device
+        self._plans: dict = {}
 
     @property
     def nbytes(self) -> int:
@@ -68,6 +74,19 @@ class DeviceCSR:
 
     def ptrs(self):
         return self.row_ptr.data_ptr(), self.col_idx.data_ptr(), self.values.data_ptr()
+
+    def plan(self, variant: int, K: int, stream: torch.cuda.Stream | None = None) -> "SpmmPlan":
+        """The cached plan of (variant, K), created (and bound on `stream`) on first use."""
+        key = (int(variant), int(K))
+        p = self._plans.get(key)
+        if p is None:
+            p = self._plans[key] = SpmmPlan(variant, self, K, stream=stream)
+        return p
+
+    def values_changed(self, stream: torch.cuda.Stream | None = None) -> None:
+        """Re-bind every cached plan after `values` changed in place."""
+        for p in self._plans.values():
+            p.bind_values(stream)
 
 
 def workspace_bytes(variant: int, m: int, nnz: int, K: int) -> int:
@@ -87,6 +106,7 @@ def _check_dense(T: torch.Tensor, rows: int, K: int, name: str) -> int:
 
 
 PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA = 1, 2, 4
+PLAN_STATS = 10  # SMFV_PLAN_STATS
 
 
 class SpmmPlan:
@@ -96,33 +116,47 @@ class SpmmPlan:
     pure asynchronous launch sequence (capturable into a hipGraph).
 
     tiles: "auto" (stage when re-use >= 3), "off", or "force".  fma: opt-in
-    fused multiply-add in the tiled kernel (SMFV_PLAN_FMA)."""
+    fused multiply-add in the tiled kernel (SMFV_PLAN_FMA).  rows=(begin,
+    end): plan of that row block only (smfv_plan_create_rows; run() writes
+    the block's rows to Y[0:end-begin]).  The values snapshot of a tiled plan
+    is gathered on `stream`; a run() on another stream waits for it."""
 
-    def __init__(self, variant: int, A: DeviceCSR, K: int, tiles: str = "auto", fma: bool = False):
+    def __init__(self, variant: int, A: DeviceCSR, K: int, tiles: str = "auto", fma: bool = False,
+                 stream: torch.cuda.Stream | None = None, rows: tuple[int, int] | None = None):
         self.variant, self.A, self.K = Variant(variant), A, K
+        self.rows = rows
         flags = {"auto": 0, "off": PLAN_NO_TILES, "force": PLAN_FORCE_TILES}[tiles]
         if fma:  # opt-in fused multiply-add in the tiled kernel: within tolerance, not bit-identical
             flags |= PLAN_FMA
         self._plan = ctypes.c_void_p()
         ip = ctypes.POINTER(ctypes.c_int)
-        call("smfv_plan_create", byref(self._plan), int(variant), A.m, A.n, A.nnz,
-             A.h_row_ptr.ctypes.data_as(ip), A.h_col_idx.ctypes.data_as(ip), K, flags)
-        self.bind_values()
+        if rows is None:
+            call("smfv_plan_create", byref(self._plan), int(variant), A.m, A.n, A.nnz,
+                 A.h_row_ptr.ctypes.data_as(ip), A.h_col_idx.ctypes.data_as(ip), K, flags)
+            self.m_out = A.m
+        else:
+            r0, r1 = int(rows[0]), int(rows[1])
+            call("smfv_plan_create_rows", byref(self._plan), int(variant), r0, r1, A.n,
+                 A.h_row_ptr.ctypes.data_as(ip), A.h_col_idx.ctypes.data_as(ip), K, flags)
+            self.m_out = r1 - r0
+        self.bind_values(stream)
 
     def bind_values(self, stream: torch.cuda.Stream | None = None) -> None:
         """(Re)bind a tiled plan to A's current device values (after they change)."""
         call("smfv_plan_bind_values", self._plan, self.A.values.data_ptr(), stream_handle(stream))
 
     def stats(self) -> dict:
-        out = (ctypes.c_double * 6)()
+        out = (ctypes.c_double * PLAN_STATS)()
         call("smfv_plan_stats", self._plan, out)
         return {"tiled": bool(out[0]), "tiles": int(out[1]), "staged_rows": int(out[2]),
-                "reuse": float(out[3]), "plan_bytes": int(out[4]), "direct_tiles": int(out[5])}
+                "reuse": float(out[3]), "plan_bytes": int(out[4]), "direct_rows": int(out[5]),
+                "row_begin": int(out[6]), "est_reuse": float(out[7]), "analysis_ms": float(out[8]),
+                "snapshot_entries": int(out[9])}
 
     def run(self, X: torch.Tensor, Y: torch.Tensor, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
         A, K = self.A, self.K
         ldx = _check_dense(X, A.n, K, "X")
-        ldy = _check_dense(Y, A.m, K, "Y")
+        ldy = _check_dense(Y, self.m_out, K, "Y")
         rp, ci, va = A.ptrs()
         call("smfv_plan_execute", self._plan, rp, ci, va, X.data_ptr(), ldx, Y.data_ptr(), ldy,
              stream_handle(stream))
@@ -139,11 +173,12 @@ class SpmmPlan:
 
 def spmm(variant: int, A: DeviceCSR, X: torch.Tensor, Y: torch.Tensor | None = None,
          stream: torch.cuda.Stream | None = None) -> torch.Tensor:
-    """Y = A * X on the device (asynchronous on `stream`)."""
+    """Y = A * X on the device (asynchronous on `stream`), through A's cached
+    plan for (variant, K)."""
     K = X.shape[1]
     if Y is None:
         Y = torch.empty((A.m, K), dtype=torch.float64, device=A.device)
-    return SpmmPlan(variant, A, K).run(X, Y, stream)
+    return A.plan(variant, K, stream).run(X, Y, stream)
 
 
 def spmm_rowblock(A: DeviceCSR, row_begin: int, row_end: int, X: torch.Tensor, Yblock: torch.Tensor,

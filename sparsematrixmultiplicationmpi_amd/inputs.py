@@ -171,3 +171,26 @@ def cop20k_surrogate(seed: int = 20) -> SparseMatrix:
     symmetric 27-point-stencil pattern on a 50x50x49 grid truncated to
     m = 121,192 rows, pair keep-probability tuned so nnz ~ 2,624,331."""
     return gen_fem27(COP20K_M, 50, 50, COP20K_KEEP, seed)
+
+
+def permute_symmetric(A: SparseMatrix, perm: np.ndarray) -> SparseMatrix:
+    """P A P^T for a square A: new row i is old row perm[i], old column c
+    becomes inv[c] (inv = perm^-1), each row sorted by column.  The same
+    matrix under another numbering (the ordering-robustness variant of the
+    cop20k_A surrogate)."""
+    perm = np.asarray(perm, dtype=np.int64)
+    m = A.numRows
+    if A.numCols != m or len(perm) != m:
+        raise ValueError("permute_symmetric needs a square matrix and a permutation of its rows")
+    inv = np.empty(m, np.int64)
+    inv[perm] = np.arange(m)
+    rp = np.asarray(A.rowPtr, np.int64)
+    lens = rp[perm + 1] - rp[perm]
+    nrp = np.zeros(m + 1, np.int64)
+    np.cumsum(lens, out=nrp[1:])
+    src = np.repeat(rp[perm] - nrp[:-1], lens) + np.arange(nrp[-1])
+    rows = np.repeat(np.arange(m), lens)
+    cols = inv[np.asarray(A.colIndices)[src]]
+    order = np.lexsort((cols, rows))
+    return SparseMatrix(values=np.asarray(A.values)[src][order], colIndices=cols[order].astype(np.int32),
+                        rowPtr=nrp.astype(np.int32), numRows=m, numCols=m)

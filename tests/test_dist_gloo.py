@@ -1,9 +1,13 @@
 """Multi-process (world_size 2 and 3, gloo, CPU) test of the distributed
-exchange logic: each rank takes its part from the NATIVE plan
-(smfv_dist_plan -- the function smfv_dist_spmm_f64 runs on the GPU path),
-computes it with the oracle, exchanges blocks with torch.distributed exactly
-as the plan lays them out (all-gatherv), assembles Y and must match the
-reference's sequential result."""
+exchange: each rank takes its part from the NATIVE plan (smfv_dist_plan --
+the function the GPU path runs), computes it with the oracle, then replays
+the NATIVE exchange schedule (smfv_dist_exchange_ops: the exact list of
+all-gather / broadcast / send / recv operations smfv_dist_spmm_f64 and the
+distributed plans issue to RCCL) with torch.distributed over gloo, assembles
+Y as the device kernels do (panels_to_rowmajor, combine_row_blocks) and must
+match the reference's sequential result -- on every rank for TO_ALL, on the
+root for TO_ROOT (the reference's MPI_Gatherv / MPI_Reduce semantics,
+SC/...RowWise.cpp:85-87, ...ColumnWise.cpp:82-84, ...NonZeroElement.cpp:88)."""
 import os
 import socket
 
@@ -25,7 +29,6 @@ def _free_port():
 def _local_part(variant, A, X, first, last, rank, p):
     from oracle import oracle
     rp, ci, va = A.rowPtr, A.colIndices, A.values
-    K = X.shape[1]
     if variant == 1:  # rows [first, last]
         sub = rp[first:last + 2] - rp[first]
         lo, hi = rp[first], rp[last + 1]
@@ -40,41 +43,66 @@ def _local_part(variant, A, X, first, last, rank, p):
     return oracle.spmm("sequential", sub, ci[s:e], va[s:e], X).reshape(-1)
 
 
-def _worker(rank, p, port, variant, q):
+def run_ops(ops, xbuf: torch.Tensor, rank: int, p: int) -> None:
+    """Replay a native exchange schedule over torch.distributed (gloo)."""
+    from sparsematrixmultiplicationmpi_amd.dist import EX_ALLGATHER, EX_BCAST, EX_RECV, EX_SEND
+    for kind, peer, off, cnt in ops:
+        if kind == EX_ALLGATHER:
+            base = off - rank * cnt
+            parts = [torch.zeros(cnt, dtype=torch.float64) for _ in range(p)]
+            dist.all_gather(parts, xbuf[off:off + cnt].clone())
+            for r in range(p):
+                xbuf[base + r * cnt: base + (r + 1) * cnt] = parts[r]
+        elif kind == EX_BCAST:
+            blk = xbuf[off:off + cnt].clone()
+            dist.broadcast(blk, src=peer)
+            xbuf[off:off + cnt] = blk
+        elif kind == EX_SEND:
+            dist.send(xbuf[off:off + cnt].clone(), dst=peer)
+        elif kind == EX_RECV:
+            blk = torch.zeros(cnt, dtype=torch.float64)
+            dist.recv(blk, src=peer)
+            xbuf[off:off + cnt] = blk
+        else:
+            raise AssertionError(kind)
+
+
+def _worker(rank, p, port, variant, mode, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=p)
         import sys
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         import sparsematrixmultiplicationmpi_amd as smfv
-        from sparsematrixmultiplicationmpi_amd.dist import exchange_plan
+        from sparsematrixmultiplicationmpi_amd.dist import TO_ALL, exchange_ops, exchange_plan
         from oracle import oracle
 
         A = smfv.gen_random_rows(900, 700, 8, 2.0, 300, 31)
         K = 6
         X = np.random.default_rng(31).uniform(-1, 1, (A.numCols, K))
         m, nnz = A.numRows, A.nnz
+        root = p - 1  # a root other than 0
         first, last, off, cnt = exchange_plan(variant, m, nnz, A.rowPtr, K, p)
         mine = _local_part(variant, A, X, first[rank], last[rank], rank, p)
         assert mine.size == cnt[rank]
-        # all-gatherv through padded all_gather
-        mx = int(cnt.max())
-        buf = torch.zeros(mx, dtype=torch.float64)
-        buf[: mine.size] = torch.from_numpy(mine)
-        parts = [torch.zeros(mx, dtype=torch.float64) for _ in range(p)]
-        dist.all_gather(parts, buf)
-        xbuf = np.zeros(int((off + cnt).max()))
-        for r in range(p):
-            xbuf[off[r]: off[r] + cnt[r]] = parts[r][: cnt[r]].numpy()
+        xbuf = torch.full((int((off + cnt).max()),), float("nan"), dtype=torch.float64)
+        xbuf[off[rank]: off[rank] + cnt[rank]] = torch.from_numpy(mine)
+        ops = exchange_ops(variant, mode, root, m, nnz, A.rowPtr, K, p, rank)
+        run_ops(ops, xbuf, rank, p)
+        if mode != TO_ALL and rank != root:
+            q.put((rank, True, "not the root"))
+            dist.destroy_process_group()
+            return
+        xb = xbuf.numpy()
         # assemble as the device code does
         if variant == 1:
-            Y = xbuf.reshape(m, K)
+            Y = xb.reshape(m, K)
         elif variant == 2:
             Y = np.zeros((m, K))
             for r in range(p):
                 kc = last[r] - first[r] + 1
                 if kc > 0:
-                    Y[:, first[r]:last[r] + 1] = xbuf[off[r]: off[r] + m * kc].reshape(m, kc)
+                    Y[:, first[r]:last[r] + 1] = xb[off[r]: off[r] + m * kc].reshape(m, kc)
         else:
             Y = np.zeros((m, K))
             seen = np.zeros(m, bool)
@@ -82,7 +110,7 @@ def _worker(rank, p, port, variant, q):
                 nr = last[r] - first[r] + 1
                 if nr <= 0:
                     continue
-                blk = xbuf[off[r]: off[r] + nr * K].reshape(nr, K)
+                blk = xb[off[r]: off[r] + nr * K].reshape(nr, K)
                 rows = slice(first[r], last[r] + 1)
                 Y[rows] = np.where(seen[rows, None], Y[rows] + blk, blk)
                 seen[rows] = True
@@ -92,40 +120,41 @@ def _worker(rank, p, port, variant, q):
             ok = err <= 1e-12
         else:
             ok = np.array_equal(Y.view(np.uint64), Yref.view(np.uint64))
-            err = float(np.max(np.abs(Y - Yref)))
-        q.put((rank, ok, err))
+            err = float(np.nanmax(np.abs(Y - Yref)))
+        q.put((rank, ok, (err, ops)))
         dist.destroy_process_group()
     except Exception as e:  # surface worker failures
         q.put((rank, False, repr(e)))
 
 
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("p", [2, 3])
 @pytest.mark.parametrize("variant", [1, 2, 3])
-def test_gloo_exchange(variant, p):
+def test_gloo_exchange(variant, p, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, p, port, variant, q)) for r in range(p)]
+    procs = [ctx.Process(target=_worker, args=(r, p, port, variant, mode, q)) for r in range(p)]
     for pr in procs:
         pr.start()
     res = [q.get(timeout=240) for _ in range(p)]
     for pr in procs:
         pr.join(timeout=60)
     for rank, ok, err in res:
-        assert ok, (variant, p, rank, err)
+        assert ok, (variant, p, mode, rank, err)
 
 
 def _rowpart_worker(rank, p, port, m, q):
     """Bench config 5's layout: rank r generates ONLY its RowWise rows
-    (counter-based generator), computes them, and the equal Y blocks are
-    all-gathered (ncclAllGather on the GPU path) into the full Y."""
+    (counter-based generator), computes them, and the native schedule
+    (one all-gather of equal blocks, else broadcasts) assembles the full Y."""
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=p)
         import sys
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         import sparsematrixmultiplicationmpi_amd as smfv
-        from sparsematrixmultiplicationmpi_amd.dist import exchange_plan
+        from sparsematrixmultiplicationmpi_amd.dist import EX_ALLGATHER, TO_ALL, exchange_ops, exchange_plan
         from oracle import oracle
 
         K = 4
@@ -134,16 +163,15 @@ def _rowpart_worker(rank, p, port, m, q):
         X = np.random.default_rng(7).uniform(-1, 1, (m, K))
         mine = oracle.spmm("sequential", A_loc.rowPtr, A_loc.colIndices, A_loc.values, X).reshape(-1)
         assert mine.size == cnt[rank] and off[rank] == first[rank] * K
-        equal = bool(np.all(cnt == cnt[0]))
-        mx = int(cnt.max())
-        buf = torch.zeros(mx, dtype=torch.float64)
-        buf[: mine.size] = torch.from_numpy(mine)
-        parts = [torch.zeros(mx, dtype=torch.float64) for _ in range(p)]
-        dist.all_gather(parts, buf)
-        Y = np.concatenate([parts[r][: cnt[r]].numpy() for r in range(p)]).reshape(m, K)
+        xbuf = torch.full((m * K,), float("nan"), dtype=torch.float64)
+        xbuf[off[rank]: off[rank] + cnt[rank]] = torch.from_numpy(mine)
+        ops = exchange_ops(1, TO_ALL, 0, m, 0, None, K, p, rank)
+        run_ops(ops, xbuf, rank, p)
+        Y = xbuf.numpy().reshape(m, K)
         A = smfv.gen_random_rows(m, m, 16.0, 0.0, 16, 42)
         Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
-        q.put((rank, bool(np.array_equal(Y.view(np.uint64), Yref.view(np.uint64))), equal))
+        single = len(ops) == 1 and ops[0][0] == EX_ALLGATHER
+        q.put((rank, bool(np.array_equal(Y.view(np.uint64), Yref.view(np.uint64))), single))
         dist.destroy_process_group()
     except Exception as e:  # surface worker failures
         q.put((rank, False, repr(e)))
@@ -162,5 +190,4 @@ def test_gloo_rowpart(p, m):
         pr.join(timeout=60)
     for rank, ok, info in res:
         assert ok, (p, m, rank, info)
-        if m % p == 0:
-            assert info is True  # equal blocks -> the single ncclAllGather path
+        assert info is (m % p == 0)  # equal blocks -> the single ncclAllGather op

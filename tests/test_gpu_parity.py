@@ -285,7 +285,8 @@ def test_tiled_plan_stats_cop20k(gpu):
     A = smfv.cop20k_surrogate()
     plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(A, gpu), 32)
     st = plan.stats()
-    assert st["reuse"] > 1.9 and st["direct_tiles"] == 0
+    assert st["reuse"] > 1.9 and st["direct_rows"] == 0
+    assert st["est_reuse"] >= 3.0 and st["tiled"]  # sampled estimate (512 tiles in the full pattern)
 
 
 def test_dist_rowpart_single_rank(gpu):
@@ -406,3 +407,147 @@ def test_spmv_stream_k1(gpu):
     S.spmm_rowblock(dA, 250, 650, torch.from_numpy(X).to(gpu), Y[250:650])
     torch.cuda.synchronize()
     assert np.array_equal(bits(Y[250:650].cpu().numpy()), bits(Yref[250:650]))
+
+
+def _forced_plan_matrix(seed):
+    """fem27 rows plus a few rows too wide for a tile (direct rows)."""
+    A = smfv.gen_random_rows(6000, 5000, 16, 2.0, 1500, seed)
+    assert np.diff(A.rowPtr).max() > 448  # some rows go to the direct list
+    return A
+
+
+@pytest.mark.parametrize("rows", [(0, 6000), (1234, 4321), (5990, 6000), (100, 100)])
+def test_plan_rowblock_tiled(gpu, rows):
+    """smfv_plan_create_rows: a rank's row block (SC/...RowWise.cpp:36-50) as
+    a tiled plan (direct rows included) -- bit-identical to the reference's
+    rows [begin, end)."""
+    A = _forced_plan_matrix(41)
+    K = 64
+    X = np.random.default_rng(41).uniform(-1, 1, (A.numCols, K))
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    dA = smfv.DeviceCSR(A, gpu)
+    r0, r1 = rows
+    for tiles in ("force", "off"):
+        plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles=tiles, rows=rows)
+        Y = torch.full((r1 - r0, K), np.nan, dtype=torch.float64, device=gpu)
+        plan.run(torch.from_numpy(X).to(gpu), Y)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref[r0:r1])), (tiles, plan.stats())
+        if tiles == "force" and r1 > r0:
+            assert plan.stats()["tiled"] and plan.stats()["row_begin"] == r0
+
+
+def test_plan_bind_on_other_stream(gpu):
+    """a tiled plan bound on one stream and run on a fresh stream
+    with no synchronisation in between waits for the values snapshot."""
+    A = _forced_plan_matrix(43)
+    K = 32
+    X = torch.from_numpy(np.random.default_rng(43).uniform(-1, 1, (A.numCols, K))).to(gpu)
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X.cpu().numpy())
+    dA = smfv.DeviceCSR(A, gpu)
+    torch.cuda.synchronize()
+    s_bind, s_run = torch.cuda.Stream(), torch.cuda.Stream()
+    for _ in range(3):
+        with torch.cuda.stream(s_bind):
+            torch.cuda._sleep(2_000_000)  # keep the bind stream busy: the gather runs late
+        plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles="force", stream=s_bind)
+        Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+        plan.run(X, Y, stream=s_run)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref))
+
+
+def test_plan_values_snapshot_contract(gpu):
+    """ADVICE r1 / include/smfv.h values contract: a tiled plan computes with
+    the values bound last -- for the tiles AND the direct rows (no mixing) --
+    until values_changed() re-binds; then it sees the new values."""
+    A = _forced_plan_matrix(47)
+    K = 32
+    X = np.random.default_rng(47).uniform(-1, 1, (A.numCols, K))
+    Y_old = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    A2 = smfv.SparseMatrix(A.values * 2.0 - 0.25, A.colIndices, A.rowPtr, A.numRows, A.numCols)
+    Y_new = oracle.spmm("sequential", A2.rowPtr, A2.colIndices, A2.values, X)
+    dA = smfv.DeviceCSR(A, gpu)
+    dX = torch.from_numpy(X).to(gpu)
+    dA.plan(smfv.Variant.ROWWISE, K)  # the cached (auto) plan
+    forced = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles="force")
+    assert forced.stats()["tiled"] and forced.stats()["direct_rows"] > 0
+    dA._plans[("forced", K)] = forced
+    dA.values.mul_(2.0).sub_(0.25)  # in place, same address, no re-bind
+    Y = torch.empty((A.numRows, K), dtype=torch.float64, device=gpu)
+    forced.run(dX, Y)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(Y.cpu().numpy()), bits(Y_old))  # the bound snapshot, all rows
+    dA.values_changed()
+    forced.run(dX, Y)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(Y.cpu().numpy()), bits(Y_new))
+    # the cached plan (through spmm) sees the new values too
+    assert np.array_equal(bits(smfv.spmm(smfv.Variant.ROWWISE, dA, dX).cpu().numpy()), bits(Y_new))
+
+
+def test_dist_plan_single_rank(gpu):
+    """Distributed plans (smfv_dist_plan_*) at one rank: every variant and
+    mode, the rank-local share tiled where it pays; plus the row-partitioned
+    plan (config 5's layout).  The exchange schedule is empty at p = 1; its
+    p > 1 form is replayed over gloo in test_dist_gloo.py."""
+    from sparsematrixmultiplicationmpi_amd import dist as D
+    comm = D.Communicator(0, 1, D.Communicator.new_unique_id())
+    A = smfv.gen_fem27(5000, 12, 12, 0.83, 53)
+    K = 32
+    X = np.random.default_rng(53).uniform(-1, 1, (A.numCols, K))
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    dA = smfv.DeviceCSR(A, gpu)
+    dX = torch.from_numpy(X).to(gpu)
+    for v in (smfv.Variant.ROWWISE, smfv.Variant.COLUMNWISE, smfv.Variant.NONZERO):
+        for to_all in (False, True):
+            for tiles in ("auto", "force"):
+                P = D.DistPlan(comm, v, dA, K, to_all, tiles=tiles)
+                Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+                P.run(dX, Y)
+                torch.cuda.synchronize()
+                Yh = Y.cpu().numpy()
+                if v == smfv.Variant.NONZERO:
+                    assert np.max(np.abs(Yh - Yref)) <= 1e-10
+                else:
+                    assert np.array_equal(bits(Yh), bits(Yref)), (v, to_all, tiles)
+                    if tiles == "force":
+                        assert P.stats()["tiled"]
+    P = D.DistPlan(comm, smfv.Variant.ROWWISE, dA, K, True, tiles="force", rowpart=True, m=A.numRows)
+    Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+    P.run_local(dX, Y)
+    P.exchange(Y)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref))
+    comm.close()
+
+
+def test_columnwise_single_pass_k128(gpu):
+    """COLUMNWISE on one device: every K panel of a row in one pass over its
+    CSR (no per-panel re-launch); bit-identical at K = 8, 40 (odd panel
+    split) and 128, with and without the tiled plan."""
+    A = smfv.gen_fem27(4000, 12, 12, 0.83, 59)
+    for K in (8, 40, 128):
+        X = np.random.default_rng(K).uniform(-1, 1, (A.numCols, K))
+        Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+        assert np.array_equal(bits(run(smfv.Variant.COLUMNWISE, A, X, gpu)), bits(Yref)), K
+
+
+def test_permuted_cop20k_surrogate(gpu):
+    """The cop20k_A surrogate under a random symmetric permutation (the same
+    matrix, another numbering): the plan still tiles it (re-use estimated in
+    the full pattern) and the result is bit-identical to the reference."""
+    A = smfv.cop20k_surrogate()
+    perm = np.random.default_rng(2024).permutation(A.numRows)
+    B = smfv.inputs.permute_symmetric(A, perm)
+    K = 32
+    X = smfv.generateLargeFatVector(B.numCols, K)
+    Yref = oracle.spmm("sequential", B.rowPtr, B.colIndices, B.values, X)
+    dB = smfv.DeviceCSR(B, gpu)
+    plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dB, K)
+    st = plan.stats()
+    assert st["tiled"] and st["est_reuse"] >= 3.0 and st["reuse"] >= 5.0, st
+    Y = torch.full((B.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+    plan.run(torch.from_numpy(X).to(gpu), Y)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref))
