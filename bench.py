@@ -11,10 +11,15 @@ rotates over enough copies of (A, X, Y) that every launch streams from HBM
 rather than from the 256 MiB Infinity Cache (cold); the same-copy (warm)
 rate is reported beside it.
 
-N > 1 (one process per GPU, launched by torch.distributed.run): every rank
-runs its own shard of the batch (an independent copy of the problem), no
-collective on the data path -> weak scaling; value = sum over ranks of the
-problems processed / the max-over-ranks time.
+N > 1 (one process per GPU, launched by torch.distributed.run): ONE problem
+decomposed over the ranks as the reference's RowWise does
+(SC/...RowWise.cpp:26-29): each rank runs its row block (a tiled plan where
+the pattern re-uses X rows), then one RCCL all-gather of the Y blocks over
+xGMI (the reference's MPI_Gatherv, :85-87) -> strong scaling; value = the
+problem's flops / the max-over-ranks time of (kernel + exchange).  The
+rank-local kernel time and the exchange are reported separately, and the
+independent-copy rate (every rank its own whole problem, no collective) as a
+secondary field.  --mode replicas makes that the value instead.
 
 cop20k_A.mtx (SuiteSparse) is not available offline: unless --mtx points at
 it, the matrix is the labelled surrogate of inputs.cop20k_surrogate() (same
@@ -41,7 +46,17 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-METRIC = "effective GFLOP/s + achieved HBM GB/s, cop20k_A × K=32, 1/2/4/8 GPUs"
+HEADLINE_METRIC = "effective GFLOP/s + achieved HBM GB/s, cop20k_A × K=32, 1/2/4/8 GPUs"
+
+
+def metric_for(config: str, K: int, variant: str) -> str:
+    """BASELINE.json's metric on its headline config; the same quantities,
+    labelled with the config actually run, on the others."""
+    if config == "cop20k_k32" and variant == "ROWWISE":
+        return HEADLINE_METRIC
+    what = {"cop20k": "cop20k_A", "pow10m": "synthetic 10M x 10M power-law", "syn80m": "synthetic 80M x 80M",
+            "cop20k_perm": "cop20k_A (randomly permuted)"}[CONFIGS[config][0]]
+    return f"effective GFLOP/s + achieved HBM GB/s, {what} × K={K}, {variant}"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MPIEXEC = "/opt/conda/bin/mpiexec"
 
@@ -51,6 +66,9 @@ CONFIGS = {
     "cop20k_k128": ("cop20k", 128, "ROWWISE"),
     "cop20k_k1": ("cop20k", 1, "SEQUENTIAL"),
     "pow10m_k32": ("pow10m", 32, "NONZERO"),
+    "pow10m_k1": ("pow10m", 1, "SEQUENTIAL"),  # K = 1 on power-law rows (k_spmv_stream long rows)
+    # the headline matrix under a random symmetric permutation (ordering robustness)
+    "cop20k_perm_k32": ("cop20k_perm", 32, "ROWWISE"),
     # config 5: 80M x 80M, 16 nnz/row, row-partitioned over the ranks + RCCL all-gather
     "syn80m_k32": ("syn80m", 32, "ROWWISE"),
 }
@@ -97,6 +115,12 @@ def build_matrix(kind: str, mtx: str | None):
         return inputs.readMatrixMarketFile(mtx), f"{os.path.basename(mtx)}"
     if kind == "cop20k":
         return inputs.cop20k_surrogate(), "cop20k_A surrogate (fem27, m=121192, symmetric)"
+    if kind == "cop20k_perm":
+        import numpy as np
+        A = inputs.cop20k_surrogate()
+        perm = np.random.default_rng(2024).permutation(A.numRows)
+        return (inputs.permute_symmetric(A, perm),
+                "cop20k_A surrogate under a random symmetric permutation (seed 2024)")
     if kind == "pow10m":
         m = 10_000_000
         return (inputs.gen_random_rows(m, m, 16.0, 2.0, 4096, 42),
@@ -227,20 +251,109 @@ def vendor_leg(copies, args, timed, flops: float):
 
 
 # ---------------------------------------------------------------------------
+# sampled result check (configs whose full reference result is too large)
+# ---------------------------------------------------------------------------
+def sampled_check(A, rows, dX, Ydev, exact: bool, row_base: int = 0) -> dict:
+    """Recompute the sampled rows on the host in the reference's order (per
+    row, non-zeros ascending, y += a * x with separate multiply and add:
+    SC/SparseMatrixFatVectorMultiply.cpp:17-27) and compare with the
+    device result: bit for bit (exact) or within 1e-12 x sum|a||x|
+    (NONZERO's reassociated sums).  rows are A's local rows; Ydev row
+    (row - row_base) holds row `row`.  Runs after the timed region."""
+    import numpy as np
+    import torch
+    from sparsematrixmultiplicationmpi_amd import sampling
+    t0 = time.time()
+    srp, scol, sval, ucols = sampling.sub_csr(A.rowPtr, A.colIndices, A.values, rows)
+    Xs = dX[torch.from_numpy(ucols).to(dX.device)].cpu().numpy()
+    K = Xs.shape[1]
+    lens = np.diff(srp.astype(np.int64))
+    acc = np.zeros((len(rows), K))
+    scale = np.zeros((len(rows), K))
+    for j in range(int(lens.max()) if len(lens) else 0):  # position j of every row, in CSR order
+        live = np.flatnonzero(lens > j)
+        e = srp[live].astype(np.int64) + j
+        prod = sval[e][:, None] * Xs[scol[e]]
+        acc[live] = acc[live] + prod
+        scale[live] = scale[live] + np.abs(prod)
+    Ys = Ydev[torch.from_numpy(np.asarray(rows) - row_base).to(Ydev.device)].cpu().numpy()
+    if exact:
+        ok = bool(np.array_equal(Ys.view(np.uint64), acc.view(np.uint64)))
+        err = float(np.max(np.abs(Ys - acc))) if len(rows) else 0.0
+    else:
+        rel = np.abs(Ys - acc) / np.maximum(scale, 1e-300)
+        err = float(rel.max()) if len(rows) else 0.0
+        ok = bool(err <= 1e-12)
+    return {"rows_checked": int(len(rows)), "ok": ok, "max_err": err,
+            "criterion": "bit-identical" if exact else "|y - y_ref| <= 1e-12 x sum|a||x|",
+            "sample": "longest rows, merge-team boundary (carry) rows, empty, first/last, random",
+            "seconds": round(time.time() - t0, 1)}
+
+
+def _timed_events(fn, world: int):
+    """HIP events on the current stream around fn(), bracketed by a barrier +
+    synchronize on both sides (max over ranks is taken by the caller)."""
+    import torch
+    import torch.distributed as dist
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0.record()
+    fn()
+    e1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return e0.elapsed_time(e1)
+
+
+def _graph_or_eager(step, steps: int, world: int):
+    """Time `steps` calls of step(i): captured into one hipGraph and replayed
+    (RCCL calls included) when capture works, else launched eagerly.
+    Returns (ms per step, how)."""
+    import torch
+    try:
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                for i in range(steps):
+                    step(i)
+        torch.cuda.current_stream().wait_stream(side)
+        g.replay()
+        torch.cuda.synchronize()
+        return _timed_events(g.replay, world) / steps, "hipGraph replay"
+    except Exception as e:  # capture refused (e.g. a collective that cannot be captured)
+        torch.cuda.synchronize()
+        print(f"[bench] graph capture failed ({e!r:.120}); timing eager launches", file=sys.stderr)
+        for i in range(3):
+            step(i)
+
+        def run():
+            for i in range(steps):
+                step(i)
+        return _timed_events(run, world) / steps, "eager launches"
+
+
 def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
     """BASELINE config 5: synthetic m x m (m = 80M), 16 uniform-random
     columns per row (splitmix64, seed 42), X = hash integers 1..100 (seed 43).
     Rank r generates ONLY its rows of the RowWise partition
     (SC/...RowWise.cpp:26-29) and holds X (n x K, 20.5 GB) replicated and
     Y (m x K) whole; a step = its row-block SpMM + the RowWise exchange as
-    one ncclAllGather of the equal Y blocks over xGMI
-    (smfv_dist_rowpart_spmm_f64).  The problem is fixed as N grows (strong
-    scaling).  Timed eagerly (RCCL inside the step)."""
+    one ncclAllGather of the equal Y blocks over xGMI (a row-partitioned
+    distributed plan, smfv_dist_plan_create_rowpart).  The problem is fixed
+    as N grows (strong scaling).  After timing, a row sample is checked bit
+    for bit against a host recomputation (rank 0: its own rows plus rows of
+    every other rank's block, regenerated alone)."""
+    import numpy as np
     import torch
     import torch.distributed as dist
     import sparsematrixmultiplicationmpi_amd as smfv
     from sparsematrixmultiplicationmpi_amd import dist as D
-    from sparsematrixmultiplicationmpi_amd import inputs
+    from sparsematrixmultiplicationmpi_amd import inputs, sampling
 
     m = n = args.rows or SYN80M_ROWS
     cpu = None
@@ -263,34 +376,34 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
         dist.init_process_group("gloo")
     comm = D.Communicator.from_torch_distributed()
     dA = smfv.DeviceCSR(A, dev)
-    del A
     X = torch.empty((n, K), dtype=torch.float64, device=dev)
     smfv.fill_x_hash(X, 43)
     Y = torch.empty((m, K), dtype=torch.float64, device=dev)
-    local_plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles="off")
-    Yloc = Y[r0:r1]
+    t0 = time.time()
+    plan = D.DistPlan(comm, smfv.Variant.ROWWISE, dA, K, to_all=True, rowpart=True, m=m)
     torch.cuda.synchronize()
-
-    def timed(fn, steps):
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(steps):
-            fn()
-        e1.record()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        return e0.elapsed_time(e1) / steps
-
-    step = lambda: D.dist_rowpart_spmm(comm, m, dA, X, Y, to_all=True)
-    kern = lambda: local_plan.run(X, Yloc)
+    t_plan = time.time() - t0
     for _ in range(args.warmup):
-        step()
-    ms_step = timed(step, args.steps)
-    ms_kern = timed(kern, args.steps)
+        plan.run(X, Y)
+    torch.cuda.synchronize()
+    # eager (the step holds an RCCL collective); ~65 ms per step at N = 1
+    ms_step = _timed_events(lambda: [plan.run(X, Y) for _ in range(args.steps)], world) / args.steps
+    ms_kern = _timed_events(lambda: [plan.run_local(X, Y) for _ in range(args.steps)], world) / args.steps
+    # sampled check, outside the timed region: rank 0's rows + rows of the other blocks
+    plan.run(X, Y)
+    torch.cuda.synchronize()
+    chk = None
+    if rank == 0:
+        rows = sampling.sample_rows(A.rowPtr, K, n_random=2000)
+        chk = sampled_check(A, rows, X, Y, exact=True, row_base=-r0)
+        other_ok, other_n = True, 0
+        for r in range(1, world):
+            for g in np.random.default_rng(r).integers(int(first[r]), int(last[r]) + 1, 16):
+                B = inputs.gen_random_rows(m, n, 16.0, 0.0, 16, 42, int(g), int(g) + 1)
+                c = sampled_check(B, np.array([0]), X, Y, exact=True, row_base=-int(g))
+                other_ok &= c["ok"]
+                other_n += 1
+        chk["other_blocks_rows_checked"], chk["ok"] = other_n, chk["ok"] and other_ok
     t = torch.tensor([ms_step, ms_kern, float(nnz_loc)], dtype=torch.float64)
     if world > 1:
         tn = torch.tensor([float(nnz_loc)], dtype=torch.float64)
@@ -306,7 +419,8 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
     gather_bytes = kbytes + 8 * nnz_loc * K  # random columns: one X row gathered per non-zero
     if rank == 0:
         out = {
-            "metric": METRIC, "value": round(flops / (ms_step * 1e-3) / 1e9, 3), "unit": "GFLOP/s",
+            "metric": metric_for("syn80m_k32", K, "ROWWISE"),
+            "value": round(flops / (ms_step * 1e-3) / 1e9, 3), "unit": "GFLOP/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": f"synthetic: {m}x{m}, 16 uniform-random columns/row (splitmix64 seed 42), X hash 1..100 (seed 43)",
@@ -316,18 +430,140 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
             "roofline": {"bound": "hbm", "achieved": round(kbytes / (ms_kern * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(kbytes / (ms_kern * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
-                         "kernel": kernel_label("ROWWISE", K, {}), "algorithmic_bytes_per_launch": kbytes,
+                         "kernel": kernel_label("ROWWISE", K, plan.stats()), "algorithmic_bytes_per_launch": kbytes,
                          "gather_model_GBps": round(gather_bytes / (ms_kern * 1e-3) / 1e9, 1),
                          "avg_launch_ms": round(ms_kern, 4),
                          "timing": "HIP events around eager launches (rank-local kernel alone; max over ranks)"},
             "exchange_ms": round(ms_step - ms_kern, 4),
-            "host_generation_s": round(t_gen, 1),
+            "host_generation_s": round(t_gen, 1), "plan_create_s": round(t_plan, 2),
+            "check": chk,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))
+    del plan
     comm.close()
     if world > 1:
         dist.destroy_process_group()
+    if chk is not None and not chk["ok"]:
+        sys.exit(3)
+
+
+def _x_rows_touched(A, r0: int, r1: int) -> int:
+    import numpy as np
+    lo, hi = int(A.rowPtr[r0]), int(A.rowPtr[r1])
+    return int(np.unique(np.asarray(A.colIndices[lo:hi])).size)
+
+
+def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int, variant: str) -> None:
+    """N > 1 on a matrix every rank holds (the reference's layout after its
+    broadcast, SC/main.cpp:106-143): ONE problem, decomposed like the
+    reference's variant (RowWise rows :26-29 / ColumnWise K columns / nnz
+    ranges), each rank its share as a distributed plan (tiled where it
+    pays), then the one RCCL exchange (all-gather of Y to every rank).  The
+    rank-local kernel and the exchange are timed separately too, and the
+    independent-copy (replicas) rate is reported beside."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import sparsematrixmultiplicationmpi_amd as smfv
+    from sparsematrixmultiplicationmpi_amd import dist as D
+    from sparsematrixmultiplicationmpi_amd import inputs
+
+    A, label = build_matrix(kind, args.mtx)
+    m, n, nnz = A.numRows, A.numCols, A.nnz
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo")  # control plane: barrier, max over ranks, RCCL id
+    comm = D.Communicator.from_torch_distributed()
+    X_host = inputs.generateLargeFatVector(n, K)
+    prob_bytes = algorithmic_bytes(m, n, nnz, K)
+    ncopies = max(1, min(16, math.ceil(args.cold_bytes / prob_bytes) + 1))
+    copies, t_plan = [], 0.0
+    for c in range(ncopies):
+        dA = smfv.DeviceCSR(A, dev)
+        dX = torch.from_numpy(X_host).to(dev)
+        dY = torch.zeros((m, K), dtype=torch.float64, device=dev)
+        t0 = time.time()
+        P = D.DistPlan(comm, smfv.Variant[variant], dA, K, to_all=True, tiles=args.tiles)
+        torch.cuda.synchronize()
+        t_plan += time.time() - t0
+        copies.append((P, dX, dY))
+    for i in range(args.warmup):
+        P, dX, dY = copies[i % ncopies]
+        P.run(dX, dY)
+    torch.cuda.synchronize()
+    ms_step, how = _graph_or_eager(lambda i: copies[i % ncopies][0].run(copies[i % ncopies][1],
+                                                                         copies[i % ncopies][2]), args.steps, world)
+    ms_loc, how_loc = _graph_or_eager(lambda i: copies[i % ncopies][0].run_local(copies[i % ncopies][1],
+                                                                                copies[i % ncopies][2]),
+                                      args.steps, world)
+    # correctness after timing: every rank's Y is the whole product (TO_ALL)
+    P, dX, dY = copies[0]
+    dY.fill_(float("nan"))
+    P.run(dX, dY)
+    torch.cuda.synchronize()
+    ref_plan = smfv.SpmmPlan(smfv.Variant.SEQUENTIAL, P.A, K)
+    Yseq = torch.empty_like(dY)
+    ref_plan.run(dX, Yseq)
+    mabs, _ = smfv.compare(Yseq, dY)
+    ok = mabs == 0.0 if variant != "NONZERO" else mabs <= 1e-6
+    # secondary: independent copies (every rank its own whole problem)
+    reps = [(smfv.SpmmPlan(smfv.Variant[variant], Pc.A, K, tiles=args.tiles), dXc, dYc) for Pc, dXc, dYc in copies]
+    torch.cuda.synchronize()
+    ms_rep, _ = _graph_or_eager(lambda i: reps[i % ncopies][0].run(reps[i % ncopies][1], reps[i % ncopies][2]),
+                                args.steps, world)
+    first, last, _, _ = D.exchange_plan(smfv.Variant[variant], m, nnz, A.rowPtr, K, world)
+    if variant == "ROWWISE":
+        r0, r1 = int(first[rank]), int(last[rank]) + 1
+        loc_bytes = 12 * (int(A.rowPtr[r1]) - int(A.rowPtr[r0])) + 4 * (r1 - r0 + 1) + \
+            8 * _x_rows_touched(A, r0, r1) * K + 8 * (r1 - r0) * K
+    else:
+        loc_bytes = prob_bytes // world
+    t = torch.tensor([ms_step, ms_loc, ms_rep, float(loc_bytes) / max(ms_loc, 1e-9), 0.0 if ok else 1.0],
+                     dtype=torch.float64)
+    tmin = t.clone()
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(tmin, op=dist.ReduceOp.MIN)
+    ms_step, ms_loc, ms_rep, _, bad = t.tolist()
+    flops = 2.0 * nnz * K
+    st = P.stats()
+    if rank == 0:
+        loc_gbps = float(tmin[3]) * 1e-6  # the slowest rank's local bytes / its local time (GB/s)
+        out = {
+            "metric": metric_for(args.config, K, variant),
+            "value": round(flops / (ms_step * 1e-3) / 1e9, 3),
+            "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 6), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f64",
+            "data": f"synthetic: {label}; X = rand()%100+1 (glibc seed 1)",
+            "config": {"workload": f"{args.config}: {label} x K={K}, {variant} decomposed over {world} GPUs "
+                                   "(rank-local plan + RCCL all-gather of Y)",
+                       "m": m, "n": n, "nnz": nnz, "K": K, "variant": variant,
+                       "parallelism": f"{variant} partition over {world} ranks (SC partition formulas), "
+                                      "A and X replicated, Y all-gathered", "copies_rotated": ncopies},
+            "roofline": {"bound": "hbm", "achieved": round(loc_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(loc_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "kernel": kernel_label(variant, K, st), "algorithmic_bytes_per_launch": int(loc_bytes),
+                         "avg_launch_ms": round(ms_loc, 6),
+                         "timing": f"rank-local kernel alone ({how_loc}), slowest rank"},
+            "rank_local_ms": round(ms_loc, 6),
+            "exchange_ms": round(ms_step - ms_loc, 6),
+            "timing": how,
+            "plan": {"create_s_total": round(t_plan, 3), "tiled": st["tiled"], "reuse": round(st["reuse"], 3)},
+            "check": {"ok": not bad, "criterion": "Y on every rank vs the 1-GPU sequential plan, device compare "
+                                                  "(bit-identical; NONZERO 1e-6)"},
+            "replicas": {"note": "every rank its own whole problem, no collective (weak scaling)",
+                         "ms_per_step": round(ms_rep, 6),
+                         "value_GFLOPs": round(world * flops / (ms_rep * 1e-3) / 1e9, 3)},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out))
+    del copies, reps, P
+    comm.close()
+    dist.destroy_process_group()
+    if bad:
+        sys.exit(3)
 
 
 def main() -> None:
@@ -338,6 +574,8 @@ def main() -> None:
     ap.add_argument("--config", default="cop20k_k32", choices=sorted(CONFIGS))
     ap.add_argument("--mtx", default=os.environ.get("SMFV_COP20K_MTX"))
     ap.add_argument("--variant", default=None, choices=["SEQUENTIAL", "ROWWISE", "COLUMNWISE", "NONZERO"])
+    ap.add_argument("--mode", default="decomposed", choices=["decomposed", "replicas"],
+                    help="N > 1: one problem decomposed over the ranks (default) or one copy per rank")
     ap.add_argument("--cold-bytes", type=float, default=1.0e9,
                     help="rotate copies until this many bytes separate two uses of one copy")
     ap.add_argument("--tiles", default="auto", choices=["auto", "off", "force"],
@@ -357,14 +595,18 @@ def main() -> None:
     if kind == "syn80m":
         bench_rowpart(args, world, rank, local, K)
         return
+    if world > 1 and args.mode == "decomposed" and kind in ("cop20k", "cop20k_perm"):
+        bench_decomposed(args, world, rank, local, kind, K, variant)
+        return
 
     A, label = build_matrix(kind, args.mtx)
     m, n, nnz = A.numRows, A.numCols, A.nnz
+    cop = kind in ("cop20k", "cop20k_perm")
 
     # CPU baseline first: rank 0 at N = 1, before anything touches the GPU
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if kind == "cop20k":
+        if cop:
             cpu = cpu_baseline(A, K, variant)
         else:  # bounded stand-in: a 1M x 1M instance of the same generator (same row-length law)
             from sparsematrixmultiplicationmpi_amd import inputs
@@ -375,22 +617,22 @@ def main() -> None:
     import torch
     import torch.distributed as dist
     import sparsematrixmultiplicationmpi_amd as smfv
-    from sparsematrixmultiplicationmpi_amd import inputs
+    from sparsematrixmultiplicationmpi_amd import inputs, sampling
 
     # one process per GPU; (local % devices) also lets a 1-GPU box rehearse N > 1
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
     if world > 1:
-        # control plane only (barrier + max over ranks): the timed step has no
-        # data-path collective, every rank runs its own shard
+        # --mode replicas: control plane only (barrier + max over ranks), every
+        # rank runs its own copy of the problem
         dist.init_process_group("gloo")
 
     # ---- resident problem copies ----------------------------------------
-    X_host = inputs.generateLargeFatVector(n, K) if kind == "cop20k" else None
+    X_host = inputs.generateLargeFatVector(n, K) if cop else None
     prob_bytes = algorithmic_bytes(m, n, nnz, K)
     ncopies = max(1, min(16, math.ceil(args.cold_bytes / prob_bytes) + 1))
-    copies = []
+    copies, t_plan = [], []
     for c in range(ncopies):
         dA = smfv.DeviceCSR(A, dev)
         if X_host is not None:
@@ -399,9 +641,15 @@ def main() -> None:
             dX = torch.empty((n, K), dtype=torch.float64, device=dev)
             smfv.fill_x_hash(dX, 43)
         dY = torch.empty((m, K), dtype=torch.float64, device=dev)
-        copies.append((smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles, fma=args.fma), dX, dY))
+        torch.cuda.synchronize()
+        t0 = time.time()
+        plan = smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles, fma=args.fma)
+        torch.cuda.synchronize()
+        t_plan.append(time.time() - t0)
+        copies.append((plan, dX, dY))
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
+    # bind cost (the values snapshot gather of a tiled plan), timed on its own
+    bind_ms = _timed_events(lambda: [copies[0][0].bind_values() for _ in range(20)], 1) / 20
 
     def step(i: int, warm: bool = False):
         plan, dX, dY = copies[0 if warm else i % ncopies]
@@ -429,17 +677,7 @@ def main() -> None:
         return g
 
     def timed(g):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        e0.record()
-        g.replay()
-        e1.record()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        return e0.elapsed_time(e1)
+        return _timed_events(g.replay, world)
 
     span_ms = timed(capture(False))
     span_ms_w = timed(capture(True))
@@ -456,15 +694,35 @@ def main() -> None:
         ms_per_step, kern_ms, kern_ms_w = t.tolist()
         span_ms_w = kern_ms_w * args.steps
 
+    # result check after timing: configs 4 (sampled rows; the full reference
+    # result is too large for the host) and the cop20k configs (device compare
+    # against the untiled row kernel, bit for bit)
+    chk = None
+    plan, dX, dY = copies[0]
+    plan.run(dX, dY)
+    torch.cuda.synchronize()
+    if rank == 0 and not cop:
+        rows = sampling.sample_rows(A.rowPtr, K)
+        chk = sampled_check(A, rows, dX, dY, exact=variant != "NONZERO")
+    elif rank == 0:
+        ref = smfv.SpmmPlan(smfv.Variant.SEQUENTIAL, plan.A, K, tiles="off")
+        Yr = torch.empty_like(dY)
+        ref.run(dX, Yr)
+        mabs, _ = smfv.compare(Yr, dY)
+        ok = mabs == 0.0 if not (variant == "NONZERO" or args.fma) else mabs <= 1e-6
+        chk = {"ok": bool(ok), "max_abs_diff": mabs,
+               "criterion": "vs the untiled row kernel (pinned bit-identical to the reference by the tests)"}
+
     flops = 2.0 * nnz * K
-    kname = kernel_label(variant, K, copies[0][0].stats())
+    st = copies[0][0].stats()
+    kname = kernel_label(variant, K, st)
     traffic, traffic_src = measured_traffic(args.config, kname) if args.tiles != "force" else (None, None)
     value = world * flops / (ms_per_step * 1e-3) / 1e9
     achieved = prob_bytes / (kern_ms * 1e-3) / 1e9
     achieved_w = prob_bytes / (kern_ms_w * 1e-3) / 1e9
     if rank == 0:
         out = {
-            "metric": METRIC,
+            "metric": metric_for(args.config, K, variant),
             "value": round(value, 3),
             "unit": "GFLOP/s",
             "n_gpus": world,
@@ -475,10 +733,10 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": f"synthetic: {label}; X = rand()%100+1 (glibc seed 1)" if kind == "cop20k" else f"synthetic: {label}",
+            "data": f"synthetic: {label}; X = rand()%100+1 (glibc seed 1)" if cop else f"synthetic: {label}",
             "config": {"workload": f"{args.config}: {label} x K={K}, {variant} HIP kernel",
                        "m": m, "n": n, "nnz": nnz, "K": K, "variant": variant,
-                       "parallelism": f"{world} GPU(s), one independent problem shard per GPU",
+                       "parallelism": f"{world} GPU(s), one independent problem copy per GPU",
                        "copies_rotated": ncopies},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
@@ -489,6 +747,12 @@ def main() -> None:
                          "timing": "HIP events around one hipGraph replay of all timed launches",
                          "stream_copy_GBps": round(stream_gbps, 1),
                          "frac_of_stream_copy": round(achieved / stream_gbps, 4) if stream_gbps else None},
+            "plan": {"tiled": st["tiled"], "tiles": st["tiles"], "reuse": round(st["reuse"], 3),
+                     "est_reuse_sampled": round(st["est_reuse"], 3), "direct_rows": st["direct_rows"],
+                     "create_s": round(t_plan[0], 3), "analysis_ms": round(st["analysis_ms"], 1),
+                     "bind_ms": round(bind_ms, 4), "snapshot_entries": st["snapshot_entries"],
+                     "note": "create = host analysis + upload, once per pattern; bind = values snapshot "
+                             "gather, once per value change; neither is in the timed step"},
             "gather_model": ({"bytes_per_launch": prob_bytes + 8 * nnz * K,
                               "GBps": round((prob_bytes + 8 * nnz * K) / (kern_ms * 1e-3) / 1e9, 1),
                               "note": "random columns: one X row gathered per non-zero (SURVEY 8d config 4)"}
@@ -497,12 +761,15 @@ def main() -> None:
                      "avg_launch_ms": round(kern_ms_w, 6), "achieved_GBps": round(achieved_w, 1),
                      "GFLOPs": round(world * flops / (span_ms_w / args.steps * 1e-3) / 1e9, 3)},
             "effective_GFLOPs_per_gpu": round(flops / (ms_per_step * 1e-3) / 1e9, 3),
+            "check": chk,
             "cpu_baseline": cpu,
             "vendor_rocsparse": vendor,
         }
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+    if chk is not None and not chk["ok"]:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

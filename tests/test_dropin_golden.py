@@ -28,9 +28,9 @@ def test_dropin_golden(tmp_path, name):
     g = load_golden(name)
     A = smfv.SparseMatrix(np.asarray(g["values"], np.float64), np.asarray(g["col_idx"], np.int32),
                           np.asarray(g["row_ptr"], np.int32), int(g["m"]), int(g["n"]))
-    smfv.write_csr_bin(str(tmp_path / "a.bin"), A)
-    smfv.write_dense_bin(str(tmp_path / "x.bin"), g["X"])
-    smfv.write_dense_bin(str(tmp_path / "y.bin"), g["Y_seq"])
+    smfv.inputs.write_csr_bin(str(tmp_path / "a.bin"), A)
+    smfv.inputs.write_dense_bin(str(tmp_path / "x.bin"), g["X"])
+    smfv.inputs.write_dense_bin(str(tmp_path / "y.bin"), g["Y_seq"])
     r = subprocess.run([MPIEXEC, "-launcher", "fork", "-n", "1", PROG, str(tmp_path / "a.bin"),
                         str(tmp_path / "x.bin"), str(tmp_path / "y.bin")],
                        capture_output=True, text=True, timeout=120)
