@@ -580,6 +580,8 @@ def main() -> None:
                     help="rotate copies until this many bytes separate two uses of one copy")
     ap.add_argument("--tiles", default="auto", choices=["auto", "off", "force"],
                     help="row-tile LDS staging of the plan (SpmmPlan tiles=)")
+    ap.add_argument("--seeds", default="frontier", choices=["frontier", "natural"],
+                    help="tile seeding of the plan (SMFV_PLAN_NATURAL_SEEDS for natural)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rows", type=int, default=0, help="syn80m_k32: matrix rows (default 80M)")
     ap.add_argument("--no-vendor", action="store_true", help="skip the rocSPARSE comparator leg")
@@ -643,7 +645,7 @@ def main() -> None:
         dY = torch.empty((m, K), dtype=torch.float64, device=dev)
         torch.cuda.synchronize()
         t0 = time.time()
-        plan = smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles, fma=args.fma)
+        plan = smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles, fma=args.fma, seeds=args.seeds)
         torch.cuda.synchronize()
         t_plan.append(time.time() - t0)
         copies.append((plan, dX, dY))

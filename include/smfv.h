@@ -135,6 +135,11 @@ typedef struct smfv_plan_s *smfv_plan_t;
  * results differ from the reference by rounding only (well inside the 1e-6
  * relative tolerance) and are no longer bit-identical. */
 #define SMFV_PLAN_FMA 4
+/* Tiles are seeded at the oldest unassigned neighbour of the tiles built so
+ * far (a wavefront through the pattern's graph: neighbouring tiles run
+ * together on one XCD and share X rows in its L2, whatever the row
+ * numbering).  This flag seeds them in row order instead (A/B). */
+#define SMFV_PLAN_NATURAL_SEEDS 8
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
 /* Plan of the row block [row_begin, row_end) of a CSR matrix (h_row_ptr /

@@ -1371,20 +1371,22 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
         for (int i = 0; i <= m; ++i) rpl[i] = (int)(h_rp[row_begin + i] - nnz_base);
         const int *cil = h_ci + nnz_base;
         bool go = true;
+        TileCaps caps;
+        caps.frontier = !(flags & SMFV_PLAN_NATURAL_SEEDS);
         if (!(flags & SMFV_PLAN_FORCE_TILES) && m > SMFV_TILE_SAMPLE_MIN_ROWS) {
             // estimate re-use on the first tiles before the full analysis
             // (which costs O(nnz * candidates))
-            TileCaps caps;
-            caps.max_tiles = SMFV_TILE_SAMPLE_TILES;
+            TileCaps sc = caps;
+            sc.max_tiles = SMFV_TILE_SAMPLE_TILES;
             TileAnalysis T;
-            analyse_tiles(m, n, rpl.data(), cil, T, caps);
+            analyse_tiles(m, n, rpl.data(), cil, T, sc);
             p->est_reuse = T.union_rows ? (double)T.tiled_nnz / (double)T.union_rows : 0.0;
             go = p->est_reuse >= SMFV_TILE_MIN_REUSE;
         }
         if (go) {
             WsPlan W;
             std::string err;
-            if (!build_ws_plan(m, n, rpl.data(), cil, W, &err)) {
+            if (!build_ws_plan(m, n, rpl.data(), cil, W, &err, caps)) {
                 set_error("%s", err.c_str());
                 rc = SMFV_ERR_INVALID;
             } else {
@@ -1747,16 +1749,20 @@ SMFV_API int smfv_compare_f64(int m, int K, const double *d_A, int64_t lda, cons
 {
     SMFV_REQUIRE(h_out && m >= 0 && K >= 0 && lda >= K && ldb >= K, "bad argument");
     hipStream_t st = as_stream(stream);
+    // a checker, synchronous by contract: plain allocation and a blocking
+    // read-back after the stream has drained (no pageable async copy)
     unsigned long long *d_out = nullptr;
-    SMFV_HIP(hipMallocAsync(reinterpret_cast<void **>(&d_out), 2 * sizeof(unsigned long long), st));
-    SMFV_HIP(hipMemsetAsync(d_out, 0, 2 * sizeof(unsigned long long), st));
-    if ((int64_t)m * K > 0)
-        hipLaunchKernelGGL(k_compare, dim3(1024), dim3(256), 0, st, m, K, d_A, lda, d_B, ldb, d_out);
-    SMFV_LAUNCHED();
+    SMFV_HIP(hipMalloc(reinterpret_cast<void **>(&d_out), 2 * sizeof(unsigned long long)));
     unsigned long long h[2] = {0, 0};
-    SMFV_HIP(hipMemcpyAsync(h, d_out, sizeof h, hipMemcpyDeviceToHost, st));
-    SMFV_HIP(hipFreeAsync(d_out, st));
-    SMFV_HIP(hipStreamSynchronize(st));
+    hipError_t e = hipMemsetAsync(d_out, 0, 2 * sizeof(unsigned long long), st);
+    if (e == hipSuccess && (int64_t)m * K > 0) {
+        hipLaunchKernelGGL(k_compare, dim3(1024), dim3(256), 0, st, m, K, d_A, lda, d_B, ldb, d_out);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipMemcpy(h, d_out, sizeof h, hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    SMFV_HIP(e);
     std::memcpy(h_out, h, sizeof h);
     return SMFV_OK;
 }

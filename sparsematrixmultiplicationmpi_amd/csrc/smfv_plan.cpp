@@ -35,8 +35,20 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A, 
     int tile = 0;
 
     int next_free = 0;
-    for (int seed = 0; seed < m; ++seed) {
-        if (assigned[seed]) continue;
+    std::vector<int> front;  // caps.frontier: unassigned neighbours of finished tiles, oldest first
+    size_t fhead = 0;
+    for (int scan = 0; scan < m;) {
+        int seed = -1;
+        if (caps.frontier)
+            while (fhead < front.size() && seed < 0) {
+                const int r = front[fhead++];
+                if (!assigned[r]) seed = r;
+            }
+        if (seed < 0) {
+            while (scan < m && assigned[scan]) ++scan;
+            if (scan >= m) break;
+            seed = scan;
+        }
         if (caps.max_tiles > 0 && tile >= caps.max_tiles) break;
         next_free = seed + 1;
         int ucount = 0;
@@ -112,6 +124,9 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A, 
                 break;
             add_row(best);
         }
+        if (caps.frontier)
+            for (int r : cand)
+                if (!assigned[r]) front.push_back(r);
         // rows by decreasing length (build_ws_plan deals them to waves in
         // this order, so the rows of a wave have similar lengths)
         std::sort(rows.begin(), rows.end(), [&](int a, int b) {
@@ -233,11 +248,11 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
 
 }  // namespace
 
-bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::string *err)
+bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::string *err, const TileCaps &caps)
 {
     P = WsPlan();
     TileAnalysis T;
-    analyse_tiles(m, n, rp, ci, T);  // TileCaps defaults are the k_rows_ws caps
+    analyse_tiles(m, n, rp, ci, T, caps);  // TileCaps defaults are the k_rows_ws caps
 
     auto len8 = [&](int r) { return std::max(8, (rp[r + 1] - rp[r] + 7) & ~7); };
     // the length a team computes: a row ends on a whole batch of 8 or on a

@@ -67,7 +67,11 @@ struct TileAnalysis {
     int64_t padded_nnz = 0;        // length of tsrc / tlidx
 };
 
-// Clustered tiling: seed a tile at the first unassigned row, then repeatedly
+// Clustered tiling: seed a tile at the first unassigned row (or, with
+// caps.frontier, at the oldest unassigned neighbour of the tiles built so
+// far: tiles then grow as a wavefront through the pattern's graph, so
+// consecutive tiles -- which run together on one XCD -- are neighbours
+// whatever the row numbering), then repeatedly
 // add the candidate row (a column index of a row already in the tile, i.e. a
 // graph neighbour for square patterns) that adds the fewest new columns to
 // the tile's union (ties: more in-tile neighbours, more non-zeros), while
@@ -80,6 +84,7 @@ struct TileCaps {
     int maxrows = WS_ROWS;         // rows
     int pad = 8;                   // row segments padded to a multiple of this (power of 2)
     int max_tiles = 0;             // > 0: stop after this many tiles (re-use estimate on a sample)
+    bool frontier = false;         // seed each tile at the oldest unassigned neighbour of earlier tiles
 };
 void analyse_tiles(int m, int n, const int *row_ptr, const int *col_idx, TileAnalysis &out,
                    const TileCaps &caps = TileCaps());
@@ -102,6 +107,7 @@ struct WsPlan {
 // Every matrix row lands in exactly one tile or in `direct`; per-row order
 // is CSR order.  The result is verified by replaying the kernel's reads;
 // returns false (with *err) if an invariant fails.
-bool build_ws_plan(int m, int n, const int *row_ptr, const int *col_idx, WsPlan &out, std::string *err);
+bool build_ws_plan(int m, int n, const int *row_ptr, const int *col_idx, WsPlan &out, std::string *err,
+                   const TileCaps &caps = TileCaps());
 
 }  // namespace smfv

@@ -105,7 +105,7 @@ def _check_dense(T: torch.Tensor, rows: int, K: int, name: str) -> int:
     return max(int(T.stride(0)), K)
 
 
-PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA = 1, 2, 4
+PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA, PLAN_NATURAL_SEEDS = 1, 2, 4, 8
 PLAN_STATS = 10  # SMFV_PLAN_STATS
 
 
@@ -122,12 +122,15 @@ class SpmmPlan:
     is gathered on `stream`; a run() on another stream waits for it."""
 
     def __init__(self, variant: int, A: DeviceCSR, K: int, tiles: str = "auto", fma: bool = False,
-                 stream: torch.cuda.Stream | None = None, rows: tuple[int, int] | None = None):
+                 stream: torch.cuda.Stream | None = None, rows: tuple[int, int] | None = None,
+                 seeds: str = "frontier"):
         self.variant, self.A, self.K = Variant(variant), A, K
         self.rows = rows
         flags = {"auto": 0, "off": PLAN_NO_TILES, "force": PLAN_FORCE_TILES}[tiles]
         if fma:  # opt-in fused multiply-add in the tiled kernel: within tolerance, not bit-identical
             flags |= PLAN_FMA
+        if seeds == "natural":  # tiles seeded in row order (A/B of the wavefront seeding)
+            flags |= PLAN_NATURAL_SEEDS
         self._plan = ctypes.c_void_p()
         ip = ctypes.POINTER(ctypes.c_int)
         if rows is None:
