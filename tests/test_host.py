@@ -238,3 +238,27 @@ def test_mtx_reader_parallel_and_fallback(tmp_path):
     C = smfv.readMatrixMarketFile(str(p2))
     assert np.array_equal(A.rowPtr, C.rowPtr) and np.array_equal(A.colIndices, C.colIndices)
     assert np.array_equal(A.values.view(np.uint64), C.values.view(np.uint64))
+
+
+REF_SC = "/root/reference/Source Code"
+
+
+def test_relink_recipe(tmp_path):
+    """a caller compiled against the reference's own
+    headers (quoted includes resolved in the reference's directory, as
+    SC/main.cpp's are) with the drop-in struct force-included, linked to
+    libsmfv_mpi.so.  Compile + link only (running needs a GPU)."""
+    if not os.path.isdir(REF_SC):
+        pytest.skip("reference sources not present (container only)")
+    src = os.path.join(ROOT, "tests", "cpp", "relink_caller.cpp")
+    inc = os.path.join(ROOT, "include")
+    out = str(tmp_path / "caller")
+    cmd = ["g++", "-std=c++17", "-include", os.path.join(inc, "MatrixDefinitions.h"), f"-I{REF_SC}", src,
+           f"-L{PKG}", "-lsmfv_mpi", "-lsmfv", "-Wl,--allow-shlib-undefined", "-o", out]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    # without the force-include the reference's own struct is used and the
+    # caller's numRows does not exist: the recipe's -include is what makes it work
+    r2 = subprocess.run([c for c in cmd if c not in ("-include", os.path.join(inc, "MatrixDefinitions.h"))],
+                        capture_output=True, text=True)
+    assert r2.returncode != 0 and "numRows" in r2.stderr
