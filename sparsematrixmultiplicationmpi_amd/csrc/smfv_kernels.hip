@@ -438,6 +438,25 @@ template <bool NT> __device__ __forceinline__ void dma16(const void *g, unsigned
                      "s_mov_b32 m0, %0"
                      : "=&s"(keep) : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
 }
+// The same with a scalar base + 32-bit per-lane byte offset (the global
+// instructions' saddr form): the 64-bit address arithmetic per lane and
+// piece disappears (one v_add per DMA at most instead of ~15 VALU).  The
+// base must be wave-uniform; every byte addressed must lie within 4 GiB of it.
+template <bool NT> __device__ __forceinline__ void dma16s(const void *base, unsigned voff, unsigned lds_dst)
+{
+    unsigned keep;
+    const uint64_t b = (uint64_t)(uintptr_t)base;
+    const uint64_t sb = ((uint64_t)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) << 32) |
+                        (uint64_t)__builtin_amdgcn_readfirstlane((unsigned)b);
+    if constexpr (NT)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(voff), "s"(sb), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+                     "s_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(voff), "s"(sb), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
+}
 __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 }  // namespace ws
 
@@ -449,7 +468,9 @@ __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(
 // 5 staging and compute both running, decoupled (no barriers; compute reads
 // slot 0 while it is restaged: timing only, results are garbage), 6 as 2 with
 // half the X reads (the other half synthesised by a multiply; timing only)
-template <int ABL, bool FMA = false>
+// SADDR: the loaders address X, the values and the offsets by scalar base +
+// 32-bit byte offset (X and the plan's arrays each < 4 GiB; the host picks it).
+template <int ABL, bool FMA = false, bool SADDR = true>
 __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
                                                      const uint16_t *__restrict__ loff,
@@ -483,6 +504,8 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
             reinterpret_cast<d2 *>(lds + (lane >> 4) * XSLOT + WS_ZOFF)[lane & 15] = d2{0.0, 0.0};
         i4 u0, u1;
         int noff, tn, nu;
+        unsigned xo[8];                       // SADDR: byte offset of this lane's 16 B of union row uc[i]
+        const unsigned ldxb = (unsigned)(ldx * 8);
         auto fetch_record = [&](int t) {
             const int *G = grec + (int64_t)t * WS_GWORDS;
             const i4 *gu = reinterpret_cast<const i4 *>(G + 32 * wl + 8 * (lane >> 4));
@@ -500,20 +523,39 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
             const unsigned xb = lds0 + xs * XSLOT;
             const int uc[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
             const int cp = p * TILE_KP;
+            if constexpr (SADDR)
+                if (p == 0)  // per tile: the union rows' byte offsets (panels add to the scalar base)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) xo[i] = (unsigned)uc[i] * ldxb + 16u * (unsigned)(lane & 15);
             auto stage_meta = [&]() {
                 const unsigned mb = lds0 + SL_M + ms * MSLOT;
-                for (int k = wl; k * 128 < tn; k += WS_LOADERS)
-                    dma16<true>(tv + noff + 128 * k + 2 * lane, mb + M_V + k * 1024);
-                for (int k = wl; k * 512 < tn; k += WS_LOADERS)
-                    dma16<true>(loff + noff + 512 * k + 8 * lane, mb + M_L + k * 1024);
-                if (wl == WS_LOADERS - 1) dma16<true>(lrec + (int64_t)t * WS_LWORDS + 4 * lane, mb + M_R);
+                if constexpr (SADDR) {
+                    const int nf = __builtin_amdgcn_readfirstlane(noff);
+                    const double *tvb = tv + nf;
+                    const uint16_t *lb = loff + nf;
+                    for (int k = wl; k * 128 < tn; k += WS_LOADERS)
+                        dma16s<true>(tvb, 1024u * k + 16u * lane, mb + M_V + k * 1024);
+                    for (int k = wl; k * 512 < tn; k += WS_LOADERS)
+                        dma16s<true>(lb, 1024u * k + 16u * lane, mb + M_L + k * 1024);
+                    if (wl == WS_LOADERS - 1) dma16s<true>(lrec + (int64_t)t * WS_LWORDS, 16u * lane, mb + M_R);
+                } else {
+                    for (int k = wl; k * 128 < tn; k += WS_LOADERS)
+                        dma16<true>(tv + noff + 128 * k + 2 * lane, mb + M_V + k * 1024);
+                    for (int k = wl; k * 512 < tn; k += WS_LOADERS)
+                        dma16<true>(loff + noff + 512 * k + 8 * lane, mb + M_L + k * 1024);
+                    if (wl == WS_LOADERS - 1) dma16<true>(lrec + (int64_t)t * WS_LWORDS + 4 * lane, mb + M_R);
+                }
             };
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int piece = 8 * wl + i;  // 1 KiB = union rows 4*piece .. +3
                 const int u = 4 * piece + (lane >> 4);
-                if (4 * piece < nu && u < WS_UCAP)
-                    dma16<false>(X + (int64_t)uc[i] * ldx + cp + 2 * (lane & 15), xb + piece * 1024);
+                if (4 * piece < nu && u < WS_UCAP) {
+                    if constexpr (SADDR)
+                        dma16s<false>(X + cp, xo[i], xb + piece * 1024);
+                    else
+                        dma16<false>(X + (int64_t)uc[i] * ldx + cp + 2 * (lane & 15), xb + piece * 1024);
+                }
             }
             if (p == 0) stage_meta();
         };
@@ -1612,16 +1654,26 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     if (plan->ntiles > 0) {
         // one persistent block per CU; a multiple of 8 (>= 8) so every XCD's tile range has blocks
         const int blocks = std::max(8, (std::min(plan->ntiles, ncu) + 7) & ~7);
+        // scalar-base addressing when X (n rows of ldx doubles) and the
+        // snapshot each span < 4 GiB
+        const bool saddr = (uint64_t)plan->n * (uint64_t)ldx * 8u < (1ull << 32) &&
+                           (uint64_t)plan->snapshot * 8u < (1ull << 32);
 #ifdef SMFV_LAB
         static const int abl = [] {  // lab-only ablations (k_rows_ws ABL modes)
             const char *e = std::getenv("SMFV_WS_ABL");
             return e ? std::atoi(e) : 0;
         }();
+        static const bool lab_saddr = [] {  // lab A/B: SMFV_WS_SADDR=0 keeps 64-bit per-lane addresses
+            const char *e = std::getenv("SMFV_WS_SADDR");
+            return !e || std::atoi(e) != 0;
+        }();
         auto kern = plan->fma ? (abl == 2 ? k_rows_ws<2, true> : k_rows_ws<0, true>)
                   : abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3>
                   : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : abl == 6 ? k_rows_ws<6> : k_rows_ws<0>;
+        if (!(saddr && lab_saddr)) kern = plan->fma ? k_rows_ws<0, true, false> : k_rows_ws<0, false, false>;
 #else
-        auto kern = plan->fma ? k_rows_ws<0, true> : k_rows_ws<0>;
+        auto kern = saddr ? (plan->fma ? k_rows_ws<0, true> : k_rows_ws<0>)
+                          : (plan->fma ? k_rows_ws<0, true, false> : k_rows_ws<0, false, false>);
 #endif
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, st, plan->ntiles, K / TILE_KP,
                            plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
