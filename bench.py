@@ -474,7 +474,8 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
-    dist.init_process_group("gloo")  # control plane: barrier, max over ranks, RCCL id
+    if world > 1:
+        dist.init_process_group("gloo")  # control plane: barrier, max over ranks, RCCL id
     comm = D.Communicator.from_torch_distributed()
     X_host = inputs.generateLargeFatVector(n, K)
     prob_bytes = algorithmic_bytes(m, n, nnz, K)
@@ -523,8 +524,9 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     t = torch.tensor([ms_step, ms_loc, ms_rep, float(loc_bytes) / max(ms_loc, 1e-9), 0.0 if ok else 1.0],
                      dtype=torch.float64)
     tmin = t.clone()
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dist.all_reduce(tmin, op=dist.ReduceOp.MIN)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(tmin, op=dist.ReduceOp.MIN)
     ms_step, ms_loc, ms_rep, _, bad = t.tolist()
     flops = 2.0 * nnz * K
     st = P.stats()
@@ -561,7 +563,8 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
         print(json.dumps(out))
     del copies, reps, P
     comm.close()
-    dist.destroy_process_group()
+    if world > 1:
+        dist.destroy_process_group()
     if bad:
         sys.exit(3)
 
@@ -574,8 +577,9 @@ def main() -> None:
     ap.add_argument("--config", default="cop20k_k32", choices=sorted(CONFIGS))
     ap.add_argument("--mtx", default=os.environ.get("SMFV_COP20K_MTX"))
     ap.add_argument("--variant", default=None, choices=["SEQUENTIAL", "ROWWISE", "COLUMNWISE", "NONZERO"])
-    ap.add_argument("--mode", default="decomposed", choices=["decomposed", "replicas"],
-                    help="N > 1: one problem decomposed over the ranks (default) or one copy per rank")
+    ap.add_argument("--mode", default=None, choices=["decomposed", "replicas"],
+                    help="one problem decomposed over the ranks (default for N > 1; at N = 1 it runs the "
+                         "distributed plan with one rank) or one copy per rank (default for N = 1)")
     ap.add_argument("--cold-bytes", type=float, default=1.0e9,
                     help="rotate copies until this many bytes separate two uses of one copy")
     ap.add_argument("--tiles", default="auto", choices=["auto", "off", "force"],
@@ -597,7 +601,8 @@ def main() -> None:
     if kind == "syn80m":
         bench_rowpart(args, world, rank, local, K)
         return
-    if world > 1 and args.mode == "decomposed" and kind in ("cop20k", "cop20k_perm"):
+    mode = args.mode or ("decomposed" if world > 1 else "replicas")
+    if mode == "decomposed" and kind in ("cop20k", "cop20k_perm"):
         bench_decomposed(args, world, rank, local, kind, K, variant)
         return
 
