@@ -92,6 +92,8 @@ def measured_traffic(config: str, kernel: str):
 def kernel_label(variant: str, K: int, plan_stats: dict) -> str:
     if variant == "NONZERO":
         return "k_merge_flat + k_carry_fixup" if K % 32 == 0 else "k_merge + k_carry_fixup"
+    if plan_stats.get("mfma"):
+        return "k_rows_mfma"
     if plan_stats.get("tiled"):
         return "k_rows_ws"
     if K == 1:
@@ -589,6 +591,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rows", type=int, default=0, help="syn80m_k32: matrix rows (default 80M)")
     ap.add_argument("--no-vendor", action="store_true", help="skip the rocSPARSE comparator leg")
+    ap.add_argument("--mfma", action="store_true",
+                    help="time the opt-in dense-block MFMA tile kernel (SMFV_PLAN_MFMA, config 3's MFMA K-panel)")
     ap.add_argument("--fma", action="store_true",
                     help="time the opt-in FMA plans (SMFV_PLAN_FMA) instead of the bit-exact ones")
     args = ap.parse_args()
@@ -650,7 +654,8 @@ def main() -> None:
         dY = torch.empty((m, K), dtype=torch.float64, device=dev)
         torch.cuda.synchronize()
         t0 = time.time()
-        plan = smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles, fma=args.fma, seeds=args.seeds)
+        plan = smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles, fma=args.fma, seeds=args.seeds,
+                             mfma=args.mfma)
         torch.cuda.synchronize()
         t_plan.append(time.time() - t0)
         copies.append((plan, dX, dY))
@@ -716,7 +721,7 @@ def main() -> None:
         Yr = torch.empty_like(dY)
         ref.run(dX, Yr)
         mabs, _ = smfv.compare(Yr, dY)
-        ok = mabs == 0.0 if not (variant == "NONZERO" or args.fma) else mabs <= 1e-6
+        ok = mabs == 0.0 if not (variant == "NONZERO" or args.fma or args.mfma) else mabs <= 1e-6
         chk = {"ok": bool(ok), "max_abs_diff": mabs,
                "criterion": "vs the untiled row kernel (pinned bit-identical to the reference by the tests)"}
 

@@ -140,6 +140,11 @@ typedef struct smfv_plan_s *smfv_plan_t;
  * together on one XCD and share X rows in its L2, whatever the row
  * numbering).  This flag seeds them in row order instead (A/B). */
 #define SMFV_PLAN_NATURAL_SEEDS 8
+/* Opt-in (BASELINE config 3's "MFMA K-panel", kept as a measured
+ * alternative): the tiles run as dense 16 x 4 blocks of A on
+ * v_mfma_f64_16x16x4f64 (k_rows_mfma).  Sums are reassociated by the MFMA:
+ * within tolerance, not bit-identical. */
+#define SMFV_PLAN_MFMA 16
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
 /* Plan of the row block [row_begin, row_end) of a CSR matrix (h_row_ptr /
@@ -165,8 +170,9 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
  * (tiled non-zeros / staged rows), [4] plan device bytes, [5] direct rows,
  * [6] first row of the block, [7] re-use estimated on the sample tiles (-1:
  * not sampled), [8] host analysis + upload time (ms), [9] values gathered
- * by each bind (snapshot entries, pads included) */
-#define SMFV_PLAN_STATS 10
+ * by each bind (snapshot entries, pads included), [10] 1 if the tiles run on
+ * the MFMA kernel (SMFV_PLAN_MFMA) */
+#define SMFV_PLAN_STATS 11
 SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS]);
 SMFV_API int smfv_plan_destroy(smfv_plan_t plan);
 

@@ -446,8 +446,9 @@ template <bool NT> __device__ __forceinline__ void dma16s(const void *base, unsi
 {
     unsigned keep;
     const uint64_t b = (uint64_t)(uintptr_t)base;
-    const uint64_t sb = ((uint64_t)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) << 32) |
-                        (uint64_t)__builtin_amdgcn_readfirstlane((unsigned)b);
+    // (readfirstlane returns int: widen through uint32_t, never sign-extend)
+    const uint64_t sb = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)(b >> 32)) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((unsigned)b);
     if constexpr (NT)
         asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\t"
                      "s_mov_b32 m0, %0"
@@ -705,6 +706,62 @@ __global__ __launch_bounds__(256) void k_rows_list(int nrows, const int *__restr
     double *y = Y + (int64_t)row * ldy + cp + 2 * tl;
     *reinterpret_cast<double2 *>(y + 16 * par) = acc0;
     *reinterpret_cast<double2 *>(y + 16 * (par ^ 1)) = acc1;
+}
+
+// ---------------------------------------------------------------------------
+// k_rows_mfma: opt-in (SMFV_PLAN_MFMA) dense-block MFMA form of the tiled
+// row kernel, the "MFMA K-panel" of BASELINE config 3, kept as a measured
+// alternative.  One 256-lane workgroup per tile (build_mfma_plan): per
+// 32-column panel the tile's union X rows are staged into LDS; wave g owns
+// rows 16g..16g+15 and, for each non-zero 16 x 4 block of A (dense, A-operand
+// lane order, zeros as pads), runs two v_mfma_f64_16x16x4f64 (columns 0-15 and
+// 16-31 of the panel) with B read from the LDS image.  Sums are reassociated
+// by the MFMA (4 terms at a time, union order): within tolerance, not
+// bit-identical.  C/D lane map of the f64 MFMA: col = lane & 15,
+// row = (lane >> 4) + 4 * reg (MI355X guide).
+// ---------------------------------------------------------------------------
+typedef double mf_d4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_rows_mfma(int npanel, const int *__restrict__ rec,
+                                                   const int *__restrict__ ucols, const int *__restrict__ bstep,
+                                                   const double *__restrict__ av, const double *__restrict__ X,
+                                                   int64_t ldx, double *__restrict__ Y, int64_t ldy)
+{
+    constexpr int UR = ((WS_UCAP + 3) / 4) * 4;  // image rows, padded to whole k-steps
+    __shared__ double xs[UR * TILE_KP];           // 60 KiB: union rows x 32 doubles
+    const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, g = tid >> 6;
+    const int *R = rec + (int64_t)t * MF_RWORDS;
+    const int *U = ucols + (int64_t)t * WS_UCAP;
+    const int nu = R[64 + 2 * MF_GROUPS];
+    const int b0 = R[64 + 2 * g], nb = R[64 + 2 * g + 1];
+    for (int p = 0; p < npanel; ++p) {
+        const int cp = p * TILE_KP;
+        if (p) __syncthreads();  // the previous panel's image is consumed
+        for (int q = tid; q < UR * 16; q += 256) {  // 16 B pieces: row q >> 4, columns 2 (q & 15)
+            const int u = q >> 4, c = 2 * (q & 15);
+            double2 v = make_double2(0.0, 0.0);
+            if (u < nu) v = *reinterpret_cast<const double2 *>(X + (int64_t)U[u] * ldx + cp + c);
+            *reinterpret_cast<double2 *>(xs + u * TILE_KP + c) = v;
+        }
+        __syncthreads();
+        mf_d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+        for (int b = 0; b < nb; ++b) {
+            const double a = __builtin_nontemporal_load(av + (int64_t)(b0 + b) * 64 + lane);
+            const int st = bstep[b0 + b];
+            const double *xr = xs + (4 * st + (lane >> 4)) * TILE_KP + (lane & 15);
+            acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, xr[0], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, xr[16], acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = R[16 * g + (lane >> 4) + 4 * r];
+            if (row >= 0) {
+                double *y = Y + (int64_t)row * ldy + cp + (lane & 15);
+                y[0] = acc0[r];
+                y[16] = acc1[r];
+            }
+        }
+    }
 }
 
 // HBM streaming probe (bench only): 16-byte vector copy, one 16-KiB chunk
@@ -1349,6 +1406,8 @@ struct smfv_plan_s {
     const double *bound_values = nullptr;  // d_values the snapshot came from
     int *ws_grec = nullptr, *ws_lrec = nullptr, *direct_rows = nullptr;
     int64_t *direct_off = nullptr;         // per direct row: its first value in tvals
+    bool mfma = false;                     // SMFV_PLAN_MFMA: k_rows_mfma (dense blocks) instead of k_rows_ws
+    int *mf_rec = nullptr, *mf_ucols = nullptr, *mf_bstep = nullptr;
     uint16_t *ws_loff = nullptr;
     void *ws = nullptr;
     size_t ws_bytes = 0, dev_bytes = 0;
@@ -1357,7 +1416,7 @@ struct smfv_plan_s {
     ~smfv_plan_s()
     {
         for (void *q : {(void *)tsrc, (void *)tvals, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
-                        (void *)direct_off, (void *)ws_loff, ws})
+                        (void *)direct_off, (void *)ws_loff, ws, (void *)mf_rec, (void *)mf_ucols, (void *)mf_bstep})
             if (q) (void)hipFree(q);
         if (bind_ev) (void)hipEventDestroy(bind_ev);
     }
@@ -1425,7 +1484,42 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
             p->est_reuse = T.union_rows ? (double)T.tiled_nnz / (double)T.union_rows : 0.0;
             go = p->est_reuse >= SMFV_TILE_MIN_REUSE;
         }
-        if (go) {
+        if (go && (flags & SMFV_PLAN_MFMA)) {
+            MfmaPlan F;
+            std::string err;
+            if (!build_mfma_plan(m, n, rpl.data(), cil, F, &err, caps)) {
+                set_error("%s", err.c_str());
+                rc = SMFV_ERR_INVALID;
+            } else {
+                p->tiled = p->mfma = true;
+                p->ntiles = F.ntiles;
+                p->union_rows = F.union_rows;
+                p->tiled_nnz = F.tiled_nnz;
+                p->ndirect = (int)F.direct.size();
+                p->reuse = F.union_rows ? (double)F.tiled_nnz / (double)F.union_rows : 0.0;
+                std::vector<int> &ts = F.tsrc;
+                for (int &q : ts)
+                    if (q >= 0) q += (int)nnz_base;
+                p->padded_nnz = (int64_t)ts.size();
+                std::vector<int64_t> doff;
+                for (int r : F.direct) {
+                    doff.push_back((int64_t)ts.size());
+                    for (int j = rpl[r]; j < rpl[r + 1]; ++j) ts.push_back((int)(nnz_base + j));
+                }
+                p->snapshot = (int64_t)ts.size();
+                if (!rc) rc = upload(&p->mf_rec, F.rec, p->dev_bytes);
+                if (!rc) rc = upload(&p->mf_ucols, F.ucols, p->dev_bytes);
+                if (!rc) rc = upload(&p->mf_bstep, F.bstep, p->dev_bytes);
+                if (!rc) rc = upload(&p->tsrc, ts, p->dev_bytes);
+                if (!rc) rc = upload(&p->direct_rows, F.direct, p->dev_bytes);
+                if (!rc) rc = upload(&p->direct_off, doff, p->dev_bytes);
+                if (!rc) {
+                    const size_t b = std::max<size_t>((size_t)p->snapshot, 1) * sizeof(double);
+                    fail_hip(hipMalloc(reinterpret_cast<void **>(&p->tvals), b), "hipMalloc(tvals)");
+                    p->dev_bytes += b;
+                }
+            }
+        } else if (go) {
             WsPlan W;
             std::string err;
             if (!build_ws_plan(m, n, rpl.data(), cil, W, &err, caps)) {
@@ -1567,7 +1661,7 @@ SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, voi
     const int64_t cnt = plan->snapshot;
     if (cnt > 0) {
         hipLaunchKernelGGL(k_gather_vals, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, cnt, plan->tsrc,
-                           d_values, plan->tvals, -0.0);
+                           d_values, plan->tvals, plan->mfma ? 0.0 : -0.0);
         SMFV_LAUNCHED();
     }
     // executes on another stream wait for this gather (smfv_plan_execute)
@@ -1609,6 +1703,7 @@ SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS])
     out[7] = plan->est_reuse;
     out[8] = plan->analysis_ms;
     out[9] = (double)plan->snapshot;
+    out[10] = plan->mfma ? 1.0 : 0.0;
     return SMFV_OK;
 }
 
@@ -1651,7 +1746,13 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         int v = 0;
         if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
     }
-    if (plan->ntiles > 0) {
+    if (plan->mfma) {
+        if (plan->ntiles > 0) {
+            hipLaunchKernelGGL(k_rows_mfma, dim3((unsigned)plan->ntiles), dim3(256), 0, st, K / TILE_KP, plan->mf_rec,
+                               plan->mf_ucols, plan->mf_bstep, plan->tvals, d_X, ldx, d_Y, ldy);
+            SMFV_LAUNCHED();
+        }
+    } else if (plan->ntiles > 0) {
         // one persistent block per CU; a multiple of 8 (>= 8) so every XCD's tile range has blocks
         const int blocks = std::max(8, (std::min(plan->ntiles, ncu) + 7) & ~7);
         // scalar-base addressing when X (n rows of ldx doubles) and the

@@ -354,4 +354,86 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     return verify_ws_plan(m, n, rp, ci, P, err);
 }
 
+// ---------------------------------------------------------------------------
+// k_rows_mfma plan
+// ---------------------------------------------------------------------------
+bool build_mfma_plan(int m, int n, const int *rp, const int *ci, MfmaPlan &P, std::string *err, const TileCaps &caps)
+{
+    P = MfmaPlan();
+    TileCaps c = caps;
+    c.ncap = 1 << 30;  // no LDS entry cap: A goes to registers block by block
+    TileAnalysis T;
+    analyse_tiles(m, n, rp, ci, T, c);
+    std::vector<int> pos((size_t)std::max(n, 1), -1), seen((size_t)std::max(n, 1), -1);
+    for (size_t t = 0; t < T.meta.size(); ++t) {
+        const TileMeta &tm = T.meta[t];
+        std::vector<int> rows;
+        for (int k = 0; k < tm.nrows; ++k) {
+            const int r = T.trows[tm.roff + k];
+            bool dup = tm.direct != 0;
+            for (int j = rp[r]; j < rp[r + 1] && !dup; ++j) {
+                if (seen[ci[j]] == r) dup = true;
+                seen[ci[j]] = r;
+            }
+            (dup ? P.direct : rows).push_back(r);
+        }
+        if (rows.empty()) continue;
+        // union in first-use order of the kept rows
+        std::vector<int> uc;
+        for (int r : rows)
+            for (int j = rp[r]; j < rp[r + 1]; ++j)
+                if (pos[ci[j]] < 0) {
+                    pos[ci[j]] = (int)uc.size();
+                    uc.push_back(ci[j]);
+                }
+        const int nu = (int)uc.size();
+        if (nu > WS_UCAP) {  // (cannot happen with WS caps; keep the invariant)
+            for (int u : uc) pos[u] = -1;
+            if (err) *err = "mfma plan: tile union over the cap";
+            return false;
+        }
+        std::vector<int> rec(MF_RWORDS, 0);
+        for (int k = 0; k < 64; ++k) rec[k] = k < (int)rows.size() ? rows[k] : -1;
+        const int nsteps = (nu + 3) / 4;
+        for (int g = 0; g < MF_GROUPS; ++g) {
+            rec[64 + 2 * g] = (int)P.blocks;
+            int cnt = 0;
+            // dense 16 x nu slice of this group: per k-step, the 64 A slots
+            std::vector<int> slot((size_t)nsteps * 64, -1);
+            for (int i = 0; i < 16; ++i) {
+                const int k = 16 * g + i;
+                if (k >= (int)rows.size()) break;
+                const int r = rows[k];
+                for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                    const int u = pos[ci[j]];
+                    slot[(size_t)(u / 4) * 64 + (u % 4) * 16 + i] = j;  // lane = row + 16 * (k within step)
+                    ++P.tiled_nnz;
+                }
+            }
+            for (int st = 0; st < nsteps; ++st) {
+                bool any = false;
+                for (int l = 0; l < 64 && !any; ++l) any = slot[(size_t)st * 64 + l] >= 0;
+                if (!any) continue;
+                P.bstep.push_back(st);
+                P.tsrc.insert(P.tsrc.end(), slot.begin() + (size_t)st * 64, slot.begin() + (size_t)(st + 1) * 64);
+                ++P.blocks;
+                ++cnt;
+            }
+            rec[64 + 2 * g + 1] = cnt;
+        }
+        rec[64 + 2 * MF_GROUPS] = nu;
+        P.rec.insert(P.rec.end(), rec.begin(), rec.end());
+        for (int q = 0; q < WS_UCAP; ++q) P.ucols.push_back(q < nu ? uc[q] : 0);
+        for (int u : uc) pos[u] = -1;
+        P.union_rows += nu;
+        ++P.ntiles;
+    }
+    std::sort(P.direct.begin(), P.direct.end());
+    if ((int64_t)P.tsrc.size() > 0x7fffffff) {
+        if (err) *err = "mfma plan: too many blocks";
+        return false;
+    }
+    return true;
+}
+
 }  // namespace smfv

@@ -110,4 +110,29 @@ struct WsPlan {
 bool build_ws_plan(int m, int n, const int *row_ptr, const int *col_idx, WsPlan &out, std::string *err,
                    const TileCaps &caps = TileCaps());
 
+// ---------------------------------------------------------------------------
+// Plan of the opt-in MFMA tile kernel k_rows_mfma (SMFV_PLAN_MFMA; within
+// tolerance, not bit-identical).  Same clustered tiles (WS caps); each tile's
+// rows in groups of 16 (one wave each); per group the 16 x union part of A is
+// cut into k-steps of 4 union columns and every non-zero 16 x 4 block is
+// stored dense in the A-operand lane order of v_mfma_f64_16x16x4f64 (lane l:
+// row l & 15, union column 4s + (l >> 4)), zeros as pads.  Rows with a
+// repeated column (the dense block would have to sum them) or over a cap go
+// to the direct list (k_rows_list, CSR order).
+// ---------------------------------------------------------------------------
+constexpr int MF_GROUPS = 4;                       // 16-row groups per tile (64 rows)
+constexpr int MF_RWORDS = 64 + 2 * MF_GROUPS + 4;  // record: rows[64], (blk_off, blk_cnt) per group, nu, pad
+
+struct MfmaPlan {
+    int ntiles = 0;
+    std::vector<int> rec;      // MF_RWORDS per tile (rows: -1 none)
+    std::vector<int> ucols;    // WS_UCAP per tile: union ids (0 past nu)
+    std::vector<int> bstep;    // per block: its k-step
+    std::vector<int> tsrc;     // 64 per block: CSR index of the A value (-1: zero)
+    std::vector<int> direct;   // rows gathered directly
+    int64_t blocks = 0, tiled_nnz = 0, union_rows = 0;
+};
+bool build_mfma_plan(int m, int n, const int *row_ptr, const int *col_idx, MfmaPlan &out, std::string *err,
+                     const TileCaps &caps = TileCaps());
+
 }  // namespace smfv

@@ -105,8 +105,8 @@ def _check_dense(T: torch.Tensor, rows: int, K: int, name: str) -> int:
     return max(int(T.stride(0)), K)
 
 
-PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA, PLAN_NATURAL_SEEDS = 1, 2, 4, 8
-PLAN_STATS = 10  # SMFV_PLAN_STATS
+PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA, PLAN_NATURAL_SEEDS, PLAN_MFMA = 1, 2, 4, 8, 16
+PLAN_STATS = 11  # SMFV_PLAN_STATS
 
 
 class SpmmPlan:
@@ -123,7 +123,7 @@ class SpmmPlan:
 
     def __init__(self, variant: int, A: DeviceCSR, K: int, tiles: str = "auto", fma: bool = False,
                  stream: torch.cuda.Stream | None = None, rows: tuple[int, int] | None = None,
-                 seeds: str = "frontier"):
+                 seeds: str = "frontier", mfma: bool = False):
         self.variant, self.A, self.K = Variant(variant), A, K
         self.rows = rows
         flags = {"auto": 0, "off": PLAN_NO_TILES, "force": PLAN_FORCE_TILES}[tiles]
@@ -131,6 +131,8 @@ class SpmmPlan:
             flags |= PLAN_FMA
         if seeds == "natural":  # tiles seeded in row order (A/B of the wavefront seeding)
             flags |= PLAN_NATURAL_SEEDS
+        if mfma:  # opt-in dense-block MFMA tile kernel: within tolerance, not bit-identical
+            flags |= PLAN_MFMA
         self._plan = ctypes.c_void_p()
         ip = ctypes.POINTER(ctypes.c_int)
         if rows is None:
@@ -154,7 +156,7 @@ class SpmmPlan:
         return {"tiled": bool(out[0]), "tiles": int(out[1]), "staged_rows": int(out[2]),
                 "reuse": float(out[3]), "plan_bytes": int(out[4]), "direct_rows": int(out[5]),
                 "row_begin": int(out[6]), "est_reuse": float(out[7]), "analysis_ms": float(out[8]),
-                "snapshot_entries": int(out[9])}
+                "snapshot_entries": int(out[9]), "mfma": bool(out[10])}
 
     def run(self, X: torch.Tensor, Y: torch.Tensor, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
         A, K = self.A, self.K

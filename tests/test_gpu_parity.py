@@ -551,3 +551,23 @@ def test_permuted_cop20k_surrogate(gpu):
     plan.run(torch.from_numpy(X).to(gpu), Y)
     torch.cuda.synchronize()
     assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref))
+
+
+@pytest.mark.parametrize("K", [32, 128])
+def test_mfma_tile_kernel_within_tolerance(gpu, K):
+    """Opt-in SMFV_PLAN_MFMA (k_rows_mfma, config 3's MFMA K-panel):
+    dense 16 x 4 blocks on v_mfma_f64_16x16x4f64, reassociated sums, within
+    1e-12 x sum|a||x| of the reference; a row with a repeated column (the
+    pat4x6 duplicate) goes to the direct list and stays exact."""
+    for A in (smfv.gen_fem27(5000, 12, 12, 0.83, 61),
+              smfv.readMatrixMarketFile(__import__("os").path.join(__import__("os").path.dirname(__file__),
+                                                                   "golden", "pat4x6.mtx"))):
+        X = np.random.default_rng(K).uniform(-1, 1, (A.numCols, K))
+        Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+        scale = oracle.spmm("sequential", A.rowPtr, A.colIndices, np.abs(A.values), np.abs(X))
+        plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(A, gpu), K, tiles="force", mfma=True)
+        assert plan.stats()["mfma"]
+        Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+        plan.run(torch.from_numpy(X).to(gpu), Y)
+        torch.cuda.synchronize()
+        assert np.all(np.abs(Y.cpu().numpy() - Yref) <= 1e-12 * scale + 1e-300)
