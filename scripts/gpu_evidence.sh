@@ -42,6 +42,19 @@ configs)
 syn80m)
   run 900 bench_syn80m_k32.json python bench.py --config syn80m_k32 --steps 10 --warmup 2 || exit $?
   ;;
+cli)
+  # the reference CLI's path on the surrogate under rocprofv3: shows which
+  # kernels sparseMatrixFatVectorMultiply* run (k_rows_ws through the plan cache)
+  run 120 write_mtx.log python -c "import sparsematrixmultiplicationmpi_amd as s; s.writeMatrixMarketFile('/tmp/cop20k_surrogate.mtx', s.cop20k_surrogate(), symmetric=True)" || exit $?
+  export TMPDIR=/tmp
+  (cd /tmp && run 300 cli_prof.log rocprofv3 --kernel-trace --stats -d "$OUT/prof_cli" -o prof --output-format csv \
+      -- "$ROOT/sparsematrixmultiplicationmpi_amd/smfv_main" 32 /tmp/cop20k_surrogate.mtx) || exit $?
+  ;;
+ablate)
+  for e in ${ABL_LIST:-"SMFV_WS_ABL=0 SMFV_WS_ABL=1 SMFV_WS_ABL=2 SMFV_WS_ABL=3 SMFV_WS_ABL=0"}; do
+    run 240 abl_$e.json env SMFV_LAB=1 $e python bench.py --no-cpu-baseline --no-vendor || exit $?
+  done
+  ;;
 pmc)
   export TMPDIR=/tmp
   for cfg in ${PMC_CONFIGS:-cop20k_k32 pow10m_k32}; do
