@@ -591,6 +591,8 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rows", type=int, default=0, help="syn80m_k32: matrix rows (default 80M)")
     ap.add_argument("--no-vendor", action="store_true", help="skip the rocSPARSE comparator leg")
+    ap.add_argument("--no-check", action="store_true",
+                    help="report the post-timing result check but do not fail on it (lab ablations)")
     ap.add_argument("--mfma", action="store_true",
                     help="time the opt-in dense-block MFMA tile kernel (SMFV_PLAN_MFMA, config 3's MFMA K-panel)")
     ap.add_argument("--fma", action="store_true",
@@ -780,7 +782,7 @@ def main() -> None:
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
-    if chk is not None and not chk["ok"]:
+    if chk is not None and not chk["ok"] and not args.no_check:
         sys.exit(3)
 
 
