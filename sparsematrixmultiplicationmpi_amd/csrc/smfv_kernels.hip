@@ -1389,6 +1389,7 @@ constexpr double SMFV_TILE_MIN_REUSE = 3.0;
 // rows' own sub-pattern misjudges a permuted matrix).
 constexpr int SMFV_TILE_SAMPLE_TILES = 512;
 constexpr int SMFV_TILE_SAMPLE_MIN_ROWS = 16384;  // below this the full analysis runs directly
+constexpr int SMFV_WS_BLOCKS_PER_XCD = 32;        // k_rows_ws blocks per XCD on MI355X (256 CUs)
 
 struct smfv_plan_s {
     int variant = 0, m = 0, n = 0, K = 0;
@@ -1474,6 +1475,7 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
         bool go = true;
         TileCaps caps;
         caps.frontier = !(flags & SMFV_PLAN_NATURAL_SEEDS);
+        caps.split_ends = (flags & SMFV_PLAN_NO_SPLIT_ENDS) ? 0 : SMFV_WS_BLOCKS_PER_XCD;
         if (!(flags & SMFV_PLAN_FORCE_TILES) && m > SMFV_TILE_SAMPLE_MIN_ROWS) {
             // estimate re-use on the first tiles before the full analysis
             // (which costs O(nnz * candidates))

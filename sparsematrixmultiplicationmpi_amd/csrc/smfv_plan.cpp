@@ -127,6 +127,7 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A, 
         if (caps.frontier)
             for (int r : cand)
                 if (!assigned[r]) front.push_back(r);
+        A.grow.insert(A.grow.end(), rows.begin(), rows.end());
         // rows by decreasing length (build_ws_plan deals them to waves in
         // this order, so the rows of a wave have similar lengths)
         std::sort(rows.begin(), rows.end(), [&](int a, int b) {
@@ -318,23 +319,32 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         ++P.ntiles;
     };
 
-    std::vector<std::vector<int>> stack;
+    auto by_length = [&](std::vector<int> &R) {
+        std::sort(R.begin(), R.end(), [&](int a, int b) {
+            const int la = rp[a + 1] - rp[a], lb = rp[b + 1] - rp[b];
+            return la != lb ? la > lb : a < b;
+        });
+    };
+    // final tiles (growth order kept for the end-halving), in wavefront order
+    std::vector<std::vector<int>> tiles, stack;
     for (const TileMeta &tm : T.meta) {
-        std::vector<int> rows(T.trows.begin() + tm.roff, T.trows.begin() + tm.roff + tm.nrows);
+        std::vector<int> rows(T.grow.begin() + tm.roff, T.grow.begin() + tm.roff + tm.nrows);
         if (tm.direct) {
             P.direct.insert(P.direct.end(), rows.begin(), rows.end());
             continue;
         }
-        std::sort(rows.begin(), rows.end(), [&](int a, int b) {
-            const int la = rp[a + 1] - rp[a], lb = rp[b + 1] - rp[b];
-            return la != lb ? la > lb : a < b;
-        });
-        stack.assign(1, rows);
+        std::vector<int> sorted = rows;
+        by_length(sorted);
+        if (layout(sorted) <= WS_NCAP) {
+            tiles.push_back(std::move(rows));
+            continue;
+        }
+        stack.assign(1, sorted);
         while (!stack.empty()) {
             std::vector<int> R = std::move(stack.back());
             stack.pop_back();
             if (layout(R) <= WS_NCAP) {
-                emit(R);
+                tiles.push_back(std::move(R));
             } else if (R.size() == 1) {
                 P.direct.push_back(R[0]);
             } else {
@@ -343,6 +353,38 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
                 stack.emplace_back(R.begin(), R.begin() + h);
             }
         }
+    }
+    const int nb = caps.split_ends;
+    const int64_t N = (int64_t)tiles.size();
+    if (nb > 0 && N >= 8 * 3 * (int64_t)nb) {
+        // per XCD range [N x / 8, N (x + 1) / 8): its first nb tiles are cut in
+        // halves; the range grows by nb, which keeps the kernel's boundaries
+        // (N + 8 nb) x / 8 = N x / 8 + nb x aligned with the per-XCD rebuild
+        std::vector<std::vector<int>> out;
+        out.reserve((size_t)(N + 8 * nb));
+        for (int x = 0; x < 8; ++x) {
+            const int64_t a = N * x / 8, b = N * (x + 1) / 8, S = b - a + nb;
+            std::vector<std::vector<int>> range((size_t)S);
+            std::vector<char> used((size_t)S, 0);
+            for (int j = 0; j < nb; ++j) {
+                std::vector<int> &t = tiles[(size_t)(a + j)];
+                const size_t h = (t.size() + 1) / 2;
+                const int64_t last = j + ((S - 1 - j) / nb) * nb;  // block j's last unit
+                range[(size_t)j].assign(t.begin(), t.begin() + h);
+                range[(size_t)last].assign(t.begin() + h, t.end());
+                used[(size_t)j] = used[(size_t)last] = 1;
+            }
+            int64_t k = a + nb;
+            for (int64_t q = 0; q < S; ++q)
+                if (!used[(size_t)q]) range[(size_t)q] = std::move(tiles[(size_t)k++]);
+            for (auto &t : range)
+                if (!t.empty()) out.push_back(std::move(t));
+        }
+        tiles = std::move(out);
+    }
+    for (auto &R : tiles) {
+        by_length(R);
+        emit(R);
     }
     if (P.entries + WS_SLACK > 0x7fffffff) {
         if (err) *err = "ws plan: too many tile entries for int32 offsets";

@@ -58,6 +58,7 @@ struct TileMeta {
 struct TileAnalysis {
     std::vector<TileMeta> meta;
     std::vector<int> trows;        // rows of each tile (any order of the matrix rows)
+    std::vector<int> grow;         // the same rows in the order the tile grew (same offsets as trows)
     std::vector<int> rbeg;         // per tile row: tile-local start | (length << 16)
     std::vector<int> ucols;        // distinct columns of each tile, first-use order
     std::vector<int> tsrc;         // per tile-ordered non-zero: its index in the CSR arrays
@@ -85,6 +86,7 @@ struct TileCaps {
     int pad = 8;                   // row segments padded to a multiple of this (power of 2)
     int max_tiles = 0;             // > 0: stop after this many tiles (re-use estimate on a sample)
     bool frontier = false;         // seed each tile at the oldest unassigned neighbour of earlier tiles
+    int split_ends = 0;            // build_ws_plan: > 0 = blocks per XCD whose first and last tile are halves
 };
 void analyse_tiles(int m, int n, const int *row_ptr, const int *col_idx, TileAnalysis &out,
                    const TileCaps &caps = TileCaps());
@@ -104,6 +106,11 @@ struct WsPlan {
 // Tiles from analyse_tiles (WS caps), each packed into the interleaved
 // layout; a tile whose layout overflows WS_NCAP is split in two (by sorted
 // row order) until it fits; a single row that cannot fit becomes direct.
+// caps.split_ends = nb (the kernel's blocks per XCD): in each XCD's tile
+// range the first nb tiles are cut in two halves (by growth order); the
+// first halves become the blocks' first units and the second halves their
+// last units, so the unoverlapped staging of a block's first tile and the
+// unoverlapped compute of its last one are half as long.
 // Every matrix row lands in exactly one tile or in `direct`; per-row order
 // is CSR order.  The result is verified by replaying the kernel's reads;
 // returns false (with *err) if an invariant fails.
