@@ -262,3 +262,45 @@ def test_relink_recipe(tmp_path):
     r2 = subprocess.run([c for c in cmd if c not in ("-include", os.path.join(inc, "MatrixDefinitions.h"))],
                         capture_output=True, text=True)
     assert r2.returncode != 0 and "numRows" in r2.stderr
+
+
+@pytest.mark.parametrize("p", [1, 2, 4, 7, 8])
+@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_exchange_schedule_delivers_every_block(p, variant, mode):
+    """The native exchange schedule (smfv_dist_exchange_ops) simulated for
+    all p ranks at once (p up to 8, the driver's node): sends pair with
+    receives, every broadcast is issued by every rank in the same order, an
+    all-gather is issued by all ranks with equal counts, and afterwards the
+    root (TO_ROOT) or every rank (TO_ALL) holds every rank's block."""
+    from sparsematrixmultiplicationmpi_amd.dist import EX_ALLGATHER, EX_BCAST, EX_RECV, EX_SEND, exchange_ops, exchange_plan
+    A = smfv.gen_random_rows(1203, 900, 7, 2.0, 200, 5)
+    K, root = 12, p - 1
+    first, last, off, cnt = exchange_plan(variant, A.numRows, A.nnz, A.rowPtr, K, p)
+    ops = [exchange_ops(variant, mode, root, A.numRows, A.nnz, A.rowPtr, K, p, r) for r in range(p)]
+    have = [{r} for r in range(p)]  # blocks (by owner rank) each rank holds
+    block_at = {int(off[r]): r for r in range(p) if cnt[r] > 0}
+    if p == 1:
+        assert ops == [[]]
+        return
+    if any(o and o[0][0] == EX_ALLGATHER for o in ops):
+        assert all(len(o) == 1 and o[0][0] == EX_ALLGATHER and o[0][3] == cnt[0] for o in ops)
+        assert all(o[0][2] == off[r] for r, o in enumerate(ops))
+        have = [set(range(p)) for _ in range(p)]
+    else:
+        bc = [[(k, pe, of, c) for k, pe, of, c in o if k == EX_BCAST] for o in ops]
+        assert all(b == bc[0] for b in bc)  # same broadcasts, same order, on every rank
+        for k, pe, of, c in bc[0]:
+            assert block_at[of] == pe and c == cnt[pe]
+            for r in range(p):
+                have[r].add(pe)
+        sends = sorted((r, pe, of, c) for r, o in enumerate(ops) for k, pe, of, c in o if k == EX_SEND)
+        recvs = sorted((pe, r, of, c) for r, o in enumerate(ops) for k, pe, of, c in o if k == EX_RECV)
+        assert sends == recvs  # (sender, receiver, offset, count) pair up
+        for s_, r_, of, c in sends:
+            assert block_at[of] == s_ and c == cnt[s_]
+            have[r_].add(s_)
+    owners = {r for r in range(p) if cnt[r] > 0}
+    targets = range(p) if mode == 1 else [root]
+    for t in targets:
+        assert owners <= have[t], (t, owners - have[t])
