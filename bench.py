@@ -586,8 +586,8 @@ def main() -> None:
                     help="rotate copies until this many bytes separate two uses of one copy")
     ap.add_argument("--tiles", default="auto", choices=["auto", "off", "force"],
                     help="row-tile LDS staging of the plan (SpmmPlan tiles=)")
-    ap.add_argument("--no-split-ends", action="store_true",
-                    help="whole tiles first and last in every block (SMFV_PLAN_NO_SPLIT_ENDS, A/B)")
+    ap.add_argument("--split-ends", action="store_true",
+                    help="half tiles first and last in every block (SMFV_PLAN_SPLIT_ENDS, A/B; measured slower)")
     ap.add_argument("--seeds", default="frontier", choices=["frontier", "natural"],
                     help="tile seeding of the plan (SMFV_PLAN_NATURAL_SEEDS for natural)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -659,7 +659,7 @@ def main() -> None:
         torch.cuda.synchronize()
         t0 = time.time()
         plan = smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles, fma=args.fma, seeds=args.seeds,
-                             mfma=args.mfma, split_ends=not args.no_split_ends)
+                             mfma=args.mfma, split_ends=args.split_ends)
         torch.cuda.synchronize()
         t_plan.append(time.time() - t0)
         copies.append((plan, dX, dY))

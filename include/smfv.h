@@ -145,11 +145,12 @@ typedef struct smfv_plan_s *smfv_plan_t;
  * v_mfma_f64_16x16x4f64 (k_rows_mfma).  Sums are reassociated by the MFMA:
  * within tolerance, not bit-identical. */
 #define SMFV_PLAN_MFMA 16
-/* The tiled plan cuts the first tile of each of the kernel's blocks in two
- * and runs the halves first and last, halving the unoverlapped staging of a
- * block's first tile and the unoverlapped compute of its last.  This flag
- * keeps whole tiles (A/B). */
-#define SMFV_PLAN_NO_SPLIT_ENDS 32
+/* Opt-in (measured slower, kept for A/B): the tiled plan cuts the first
+ * tile of each of the kernel's blocks in two and runs the halves first and
+ * last, halving the unoverlapped staging of a block's first tile and the
+ * unoverlapped compute of its last -- at the cost of one more unit per block
+ * (26.5 -> 27.2 us on the cop20k surrogate, K = 32). */
+#define SMFV_PLAN_SPLIT_ENDS 32
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
 /* Plan of the row block [row_begin, row_end) of a CSR matrix (h_row_ptr /

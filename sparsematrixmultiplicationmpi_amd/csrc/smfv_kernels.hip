@@ -1475,7 +1475,7 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
         bool go = true;
         TileCaps caps;
         caps.frontier = !(flags & SMFV_PLAN_NATURAL_SEEDS);
-        caps.split_ends = (flags & SMFV_PLAN_NO_SPLIT_ENDS) ? 0 : SMFV_WS_BLOCKS_PER_XCD;
+        caps.split_ends = (flags & SMFV_PLAN_SPLIT_ENDS) ? SMFV_WS_BLOCKS_PER_XCD : 0;
         if (!(flags & SMFV_PLAN_FORCE_TILES) && m > SMFV_TILE_SAMPLE_MIN_ROWS) {
             // estimate re-use on the first tiles before the full analysis
             // (which costs O(nnz * candidates))

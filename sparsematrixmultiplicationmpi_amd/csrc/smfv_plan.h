@@ -106,7 +106,8 @@ struct WsPlan {
 // Tiles from analyse_tiles (WS caps), each packed into the interleaved
 // layout; a tile whose layout overflows WS_NCAP is split in two (by sorted
 // row order) until it fits; a single row that cannot fit becomes direct.
-// caps.split_ends = nb (the kernel's blocks per XCD): in each XCD's tile
+// caps.split_ends = nb (the kernel's blocks per XCD; opt-in, measured
+// slower: one more unit per block costs more than the halved ends save): in each XCD's tile
 // range the first nb tiles are cut in two halves (by growth order); the
 // first halves become the blocks' first units and the second halves their
 // last units, so the unoverlapped staging of a block's first tile and the

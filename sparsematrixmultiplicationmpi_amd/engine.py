@@ -105,7 +105,7 @@ def _check_dense(T: torch.Tensor, rows: int, K: int, name: str) -> int:
     return max(int(T.stride(0)), K)
 
 
-PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA, PLAN_NATURAL_SEEDS, PLAN_MFMA, PLAN_NO_SPLIT_ENDS = 1, 2, 4, 8, 16, 32
+PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA, PLAN_NATURAL_SEEDS, PLAN_MFMA, PLAN_SPLIT_ENDS = 1, 2, 4, 8, 16, 32
 PLAN_STATS = 11  # SMFV_PLAN_STATS
 
 
@@ -123,7 +123,7 @@ class SpmmPlan:
 
     def __init__(self, variant: int, A: DeviceCSR, K: int, tiles: str = "auto", fma: bool = False,
                  stream: torch.cuda.Stream | None = None, rows: tuple[int, int] | None = None,
-                 seeds: str = "frontier", mfma: bool = False, split_ends: bool = True):
+                 seeds: str = "frontier", mfma: bool = False, split_ends: bool = False):
         self.variant, self.A, self.K = Variant(variant), A, K
         self.rows = rows
         flags = {"auto": 0, "off": PLAN_NO_TILES, "force": PLAN_FORCE_TILES}[tiles]
@@ -133,8 +133,8 @@ class SpmmPlan:
             flags |= PLAN_NATURAL_SEEDS
         if mfma:  # opt-in dense-block MFMA tile kernel: within tolerance, not bit-identical
             flags |= PLAN_MFMA
-        if not split_ends:  # whole tiles first and last (A/B of the end-halving)
-            flags |= PLAN_NO_SPLIT_ENDS
+        if split_ends:  # opt-in: half tiles first and last in every block (A/B; measured slower)
+            flags |= PLAN_SPLIT_ENDS
         self._plan = ctypes.c_void_p()
         ip = ctypes.POINTER(ctypes.c_int)
         if rows is None:
