@@ -478,7 +478,8 @@ __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(
 // overlaps the other group's issue, so the DMA stream never empties at a
 // unit boundary (PIPE 1 drains every unit before its barrier).
 template <int ABL, bool FMA = false, bool SADDR = true, int PIPE = 1>
-__global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, const int *__restrict__ grec,
+__global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, int chunked,
+                                                     const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
                                                      const uint16_t *__restrict__ loff,
                                                      const double *__restrict__ tv,
@@ -489,13 +490,25 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, con
     __shared__ __attribute__((aligned(16))) char lds[SL_M + 2 * MSLOT];
     int t0, tstep, cnt;
     {
+        // XCD x = blockIdx.x % 8 owns tiles [first, end) of the plan's order;
+        // its nb blocks take them strided (block j: first + j, + nb, ...) or,
+        // chunked, as consecutive runs (block j: a run of q or q + 1 tiles),
+        // so a block's next tile is the wavefront neighbour of its last one
         const int nb = gridDim.x >> 3;  // blocks per XCD
         const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
         const int first = (int)((int64_t)ntiles * x / 8), end = (int)((int64_t)ntiles * (x + 1) / 8);
-        t0 = first + j;
-        tstep = nb;
-        if (t0 >= end) return;  // block-uniform
-        cnt = (end - 1 - t0) / nb + 1;
+        if (chunked) {
+            const int S = end - first, q = S / nb, r = S % nb;
+            t0 = first + j * q + min(j, r);
+            cnt = q + (j < r ? 1 : 0);
+            tstep = 1;
+            if (cnt <= 0) return;  // block-uniform
+        } else {
+            t0 = first + j;
+            tstep = nb;
+            if (t0 >= end) return;  // block-uniform
+            cnt = (end - 1 - t0) / nb + 1;
+        }
     }
     const int tlast = t0 + (cnt - 1) * tstep;
     const int nunits = cnt * npanel;
@@ -1464,6 +1477,7 @@ constexpr double SMFV_TILE_MIN_REUSE = 3.0;
 constexpr int SMFV_TILE_SAMPLE_TILES = 512;
 constexpr int SMFV_TILE_SAMPLE_MIN_ROWS = 16384;  // below this the full analysis runs directly
 constexpr int SMFV_WS_BLOCKS_PER_XCD = 32;        // k_rows_ws blocks per XCD on MI355X (256 CUs)
+constexpr int SMFV_WS_CHUNKED = 0;                // k_rows_ws tile order per block: 0 strided, 1 consecutive runs
 
 struct smfv_plan_s {
     int variant = 0, m = 0, n = 0, K = 0;
@@ -1831,6 +1845,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     } else if (plan->ntiles > 0) {
         // one persistent block per CU; a multiple of 8 (>= 8) so every XCD's tile range has blocks
         const int blocks = std::max(8, (std::min(plan->ntiles, ncu) + 7) & ~7);
+        int chunked = SMFV_WS_CHUNKED;
         // scalar-base addressing when X (n rows of ldx doubles) and the
         // snapshot each span < 4 GiB
         const bool saddr = (uint64_t)plan->n * (uint64_t)ldx * 8u < (1ull << 32) &&
@@ -1848,6 +1863,11 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             const char *e = std::getenv("SMFV_WS_PIPE");
             return e ? std::atoi(e) : 1;
         }();
+        static const int lab_chunked = [] {  // lab A/B: SMFV_WS_CHUNKED=0/1 overrides the tile order
+            const char *e = std::getenv("SMFV_WS_CHUNKED");
+            return e ? std::atoi(e) : -1;
+        }();
+        if (lab_chunked >= 0) chunked = lab_chunked;
         auto kern = plan->fma ? (abl == 2 ? k_rows_ws<2, true> : k_rows_ws<0, true>)
                   : abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3>
                   : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : abl == 6 ? k_rows_ws<6> : k_rows_ws<0>;
@@ -1857,7 +1877,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         auto kern = saddr ? (plan->fma ? k_rows_ws<0, true> : k_rows_ws<0>)
                           : (plan->fma ? k_rows_ws<0, true, false> : k_rows_ws<0, false, false>);
 #endif
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, st, plan->ntiles, K / TILE_KP,
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, st, plan->ntiles, K / TILE_KP, chunked,
                            plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();
     }
