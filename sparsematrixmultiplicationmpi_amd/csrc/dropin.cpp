@@ -327,6 +327,9 @@ std::vector<PlanEntry> &plans()
 PlanEntry &plan_for(int variant, const SparseMatrix &A, const Problem &P, int world)
 {
     static uint64_t tick = 0;
+    // on one rank SEQUENTIAL / ROWWISE / COLUMNWISE are the same computation
+    // (bit-identical per-row sums): they share one plan
+    if (world == 1 && variant != SMFV_NONZERO) variant = SMFV_ROWWISE;
     const PlanKey key{variant, P.m, P.n, P.K, world, P.nnz, P.hrp, P.hci};
     auto &v = plans();
     for (auto &e : v)

@@ -39,6 +39,7 @@ def test_cli_stdout_contract(tmp_path):
         assert f"{name}: Results are the same!" in out  # checked on the device (smfvCompareWithReference)
     # (r2) device-resident input distribution, timed on its own line
     assert re.search(r"^Input distribution time: [0-9.eE+-]+$", out, re.M)
+    assert re.search(r"^Plan setup time: [0-9.eE+-]+$", out, re.M)
     # the PETSc block's analogue (SC/main.cpp:352,388 line shapes)
     assert re.search(r"^rocSPARSE Execution time: [0-9.eE+-]+$", out, re.M)
     assert "rocSPARSE: Results are the same!" in out
