@@ -29,7 +29,8 @@ prof)
       --output-format csv -- python3 "$ROOT/bench.py" --no-cpu-baseline --steps 200 --warmup 20) || exit $?
   ;;
 configs)
-  for c in ${CONFIGS:-"cop20k_k128 cop20k_k1 pow10m_k32 pow10m_k1 cop20k_perm_k32"}; do
+  CONFIGS=${CONFIGS:-cop20k_k128 cop20k_k1 pow10m_k32 pow10m_k1 cop20k_perm_k32}
+  for c in $CONFIGS; do
     run 400 bench_$c.json python bench.py --config $c --no-cpu-baseline || exit $?
   done
   for v in COLUMNWISE NONZERO; do
@@ -51,7 +52,8 @@ cli)
       -- "$ROOT/sparsematrixmultiplicationmpi_amd/smfv_main" 32 /tmp/cop20k_surrogate.mtx) || exit $?
   ;;
 ablate)
-  for e in ${ABL_LIST:-"SMFV_WS_ABL=0 SMFV_WS_ABL=1 SMFV_WS_ABL=2 SMFV_WS_ABL=3 SMFV_WS_ABL=0"}; do
+  ABL_LIST=${ABL_LIST:-SMFV_WS_ABL=0 SMFV_WS_ABL=1 SMFV_WS_ABL=2 SMFV_WS_ABL=3 SMFV_WS_ABL=0}
+  for e in $ABL_LIST; do
     run 240 abl_$e.json env SMFV_LAB=1 $e python bench.py --no-cpu-baseline --no-vendor --no-check || exit $?
   done
   ;;
