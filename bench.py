@@ -89,7 +89,7 @@ def measured_traffic(config: str, kernel: str):
     return e["traffic_bytes_per_launch"], e["source"]
 
 
-def kernel_label(variant: str, K: int, plan_stats: dict) -> str:
+def kernel_label(variant: str, K: int, plan_stats: dict, x_bytes: int = 0) -> str:
     if variant == "NONZERO":
         return "k_merge_flat + k_carry_fixup" if K % 32 == 0 else "k_merge + k_carry_fixup"
     if plan_stats.get("mfma"):
@@ -103,7 +103,8 @@ def kernel_label(variant: str, K: int, plan_stats: dict) -> str:
     pairs = K // 2
     cfg = (16, 4, 4) if pairs >= 64 else (8, 2, 8) if pairs >= 16 else (8, 1, 8) if pairs >= 8 else \
         (4, 1, 8) if pairs >= 4 else (2, 1, 8) if pairs >= 2 else (1, 1, 8)
-    return "k_rows_mh<%d, %d, %d, true>" % cfg
+    buf = "true" if 0 < x_bytes <= 0x7FFFFFFF else "false"  # buffer-resource X gathers when X < 2 GiB
+    return "k_rows_mh<%d, %d, %d, %s>" % (cfg + (buf,))
 
 
 def algorithmic_bytes(m: int, n: int, nnz: int, K: int) -> int:
@@ -432,7 +433,8 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
             "roofline": {"bound": "hbm", "achieved": round(kbytes / (ms_kern * 1e-3) / 1e9, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(kbytes / (ms_kern * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4), "traffic": None,
-                         "kernel": kernel_label("ROWWISE", K, plan.stats()), "algorithmic_bytes_per_launch": kbytes,
+                         "kernel": kernel_label("ROWWISE", K, plan.stats(), 8 * n * K),
+                         "algorithmic_bytes_per_launch": kbytes,
                          "gather_model_GBps": round(gather_bytes / (ms_kern * 1e-3) / 1e9, 1),
                          "avg_launch_ms": round(ms_kern, 4),
                          "timing": "HIP events around eager launches (rank-local kernel alone; max over ranks)"},
@@ -548,7 +550,8 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
                                       "A and X replicated, Y all-gathered", "copies_rotated": ncopies},
             "roofline": {"bound": "hbm", "achieved": round(loc_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(loc_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
-                         "kernel": kernel_label(variant, K, st), "algorithmic_bytes_per_launch": int(loc_bytes),
+                         "kernel": kernel_label(variant, K, st, 8 * n * K),
+                         "algorithmic_bytes_per_launch": int(loc_bytes),
                          "avg_launch_ms": round(ms_loc, 6),
                          "timing": f"rank-local kernel alone ({how_loc}), slowest rank"},
             "rank_local_ms": round(ms_loc, 6),
@@ -731,7 +734,7 @@ def main() -> None:
 
     flops = 2.0 * nnz * K
     st = copies[0][0].stats()
-    kname = kernel_label(variant, K, st)
+    kname = kernel_label(variant, K, st, 8 * n * K)
     traffic, traffic_src = measured_traffic(args.config, kname) if args.tiles != "force" else (None, None)
     value = world * flops / (ms_per_step * 1e-3) / 1e9
     achieved = prob_bytes / (kern_ms * 1e-3) / 1e9
