@@ -593,6 +593,9 @@ def main() -> None:
                     help="half tiles first and last in every block (SMFV_PLAN_SPLIT_ENDS, A/B; measured slower)")
     ap.add_argument("--seeds", default="frontier", choices=["frontier", "natural"],
                     help="tile seeding of the plan (SMFV_PLAN_NATURAL_SEEDS for natural)")
+    ap.add_argument("--xcd-parts", default="auto", choices=["auto", "one"],
+                    help="XCD tile ranges of the plan: row range per XCD when the footprint allows (auto) "
+                         "or one wavefront cut in 8 (one: SMFV_PLAN_ONE_WAVEFRONT, A/B)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rows", type=int, default=0, help="syn80m_k32: matrix rows (default 80M)")
     ap.add_argument("--no-vendor", action="store_true", help="skip the rocSPARSE comparator leg")
@@ -662,7 +665,7 @@ def main() -> None:
         torch.cuda.synchronize()
         t0 = time.time()
         plan = smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles, fma=args.fma, seeds=args.seeds,
-                             mfma=args.mfma, split_ends=args.split_ends)
+                             mfma=args.mfma, split_ends=args.split_ends, xcd_parts=args.xcd_parts)
         torch.cuda.synchronize()
         t_plan.append(time.time() - t0)
         copies.append((plan, dX, dY))
@@ -770,6 +773,7 @@ def main() -> None:
                      "est_reuse_sampled": round(st["est_reuse"], 3), "direct_rows": st["direct_rows"],
                      "create_s": round(t_plan[0], 3), "analysis_ms": round(st["analysis_ms"], 1),
                      "bind_ms": round(bind_ms, 4), "snapshot_entries": st["snapshot_entries"],
+                     "xcd_parts": st["xcd_parts"], "footprint_8_ranges": round(st["footprint"], 3),
                      "note": "create = host analysis + upload, once per pattern; bind = values snapshot "
                              "gather, once per value change; neither is in the timed step"},
             "gather_model": ({"bytes_per_launch": prob_bytes + 8 * nnz * K,

@@ -151,6 +151,12 @@ typedef struct smfv_plan_s *smfv_plan_t;
  * unoverlapped compute of its last -- at the cost of one more unit per block
  * (26.5 -> 27.2 us on the cop20k surrogate, K = 32). */
 #define SMFV_PLAN_SPLIT_ENDS 32
+/* Each XCD has its own L2, so the tiled plan splits the rows into 8 parts
+ * of equal non-zero count -- row ranges, or shares of the rows' breadth-first
+ * order, whichever reads fewer X rows summed over the parts -- tiles each
+ * part as its own wavefront and runs part x on XCD x.  This flag keeps one
+ * wavefront over the whole pattern cut into 8 consecutive shares (A/B). */
+#define SMFV_PLAN_ONE_WAVEFRONT 64
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
 /* Plan of the row block [row_begin, row_end) of a CSR matrix (h_row_ptr /
@@ -169,6 +175,13 @@ SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, voi
  * [4] tile entries (incl. pads), [5] non-zeros in tiles.  No device needed. */
 SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_col_idx,
                                double out[6]);
+/* The same for the row block [row_begin, row_end) with the caps a plan of
+ * these flags uses (smfv_plan_create_rows): out[0..5] as above, [6] XCD
+ * parts (8 or 1), [7] X footprint of the 8 parts (-1: not computed),
+ * [8] X footprint of the plan's 8 XCD tile ranges (distinct X rows each
+ * reads, summed, over the block's distinct X rows).  No device needed. */
+SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int *h_row_ptr,
+                                    const int *h_col_idx, int flags, double out[9]);
 SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int *d_col_idx,
                                const double *d_values, const double *d_X, int64_t ldx,
                                double *d_Y, int64_t ldy, void *stream);
@@ -177,8 +190,10 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
  * [6] first row of the block, [7] re-use estimated on the sample tiles (-1:
  * not sampled), [8] host analysis + upload time (ms), [9] values gathered
  * by each bind (snapshot entries, pads included), [10] 1 if the tiles run on
- * the MFMA kernel (SMFV_PLAN_MFMA) */
-#define SMFV_PLAN_STATS 11
+ * the MFMA kernel (SMFV_PLAN_MFMA), [11] XCD parts (8: one part of the
+ * rows per XCD, 1: one wavefront), [12] X rows the 8 parts read, summed,
+ * over the pattern's X rows (-1: not computed) */
+#define SMFV_PLAN_STATS 13
 SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS]);
 SMFV_API int smfv_plan_destroy(smfv_plan_t plan);
 

@@ -54,6 +54,7 @@ _SIGS = {
     "smfv_plan_create_rows": (c_int, [POINTER(c_void_p), c_int, c_int, c_int, c_int, _PI, _PI, c_int,
                                       c_int]),
     "smfv_plan_analyse": (c_int, [c_int, c_int, _PI, _PI, _PD]),
+    "smfv_plan_analyse_rows": (c_int, [c_int, c_int, c_int, _PI, _PI, c_int, _PD]),
     "smfv_plan_bind_values": (c_int, [c_void_p, c_void_p, c_void_p]),
     "smfv_plan_execute": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                   c_void_p, c_int64, c_void_p]),

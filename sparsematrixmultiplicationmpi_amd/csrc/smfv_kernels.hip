@@ -477,8 +477,11 @@ __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(
 // (the group of unit u + 1 has drained: it landed).  A group's drain
 // overlaps the other group's issue, so the DMA stream never empties at a
 // unit boundary (PIPE 1 drains every unit before its barrier).
+struct WsXcd {
+    int first[9];  // XCD x runs tiles [first[x], first[x + 1]) of the plan's order
+};
 template <int ABL, bool FMA = false, bool SADDR = true, int PIPE = 1>
-__global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, int chunked,
+__global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int chunked,
                                                      const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
                                                      const uint16_t *__restrict__ loff,
@@ -490,13 +493,14 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(int ntiles, int npanel, int
     __shared__ __attribute__((aligned(16))) char lds[SL_M + 2 * MSLOT];
     int t0, tstep, cnt;
     {
-        // XCD x = blockIdx.x % 8 owns tiles [first, end) of the plan's order;
+        // XCD x = blockIdx.x % 8 owns tiles [first, end) of the plan's order
+        // (its row range, or an eighth of one wavefront: build_ws_plan);
         // its nb blocks take them strided (block j: first + j, + nb, ...) or,
         // chunked, as consecutive runs (block j: a run of q or q + 1 tiles),
         // so a block's next tile is the wavefront neighbour of its last one
         const int nb = gridDim.x >> 3;  // blocks per XCD
         const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
-        const int first = (int)((int64_t)ntiles * x / 8), end = (int)((int64_t)ntiles * (x + 1) / 8);
+        const int first = xr.first[x], end = xr.first[x + 1];
         if (chunked) {
             const int S = end - first, q = S / nb, r = S % nb;
             t0 = first + j * q + min(j, r);
@@ -1479,6 +1483,32 @@ constexpr int SMFV_TILE_SAMPLE_MIN_ROWS = 16384;  // below this the full analysi
 constexpr int SMFV_WS_BLOCKS_PER_XCD = 32;        // k_rows_ws blocks per XCD on MI355X (256 CUs)
 constexpr int SMFV_WS_CHUNKED = 0;                // k_rows_ws tile order per block: 0 strided, 1 consecutive runs
 
+// The tile caps a plan with these flags uses for the row block (row_begin,
+// m rows; rp block-local, ci from the block's first non-zero).
+static TileCaps plan_caps(int flags, int row_begin, int m, int n, const int *rp, const int *ci, double *footprint)
+{
+    TileCaps caps;
+    caps.frontier = !(flags & SMFV_PLAN_NATURAL_SEEDS);
+    caps.split_ends = (flags & SMFV_PLAN_SPLIT_ENDS) ? SMFV_WS_BLOCKS_PER_XCD : 0;
+    caps.col_base = row_begin;  // a row block's neighbours are its columns shifted by row_begin
+    *footprint = -1.0;
+    if (caps.frontier && m > 0 && !(flags & (SMFV_PLAN_ONE_WAVEFRONT | SMFV_PLAN_SPLIT_ENDS | SMFV_PLAN_MFMA))) {
+        // one part per XCD: the row ranges or the breadth-first shares,
+        // whichever reads fewer X rows over the 8 L2s
+        std::vector<int> br, bs;
+        range_parts(m, rp, 8, caps.part_rows, caps.part_start);
+        bfs_parts(m, rp, ci, row_begin, 8, br, bs);
+        const double fr = parts_footprint(m, n, rp, ci, caps.part_rows, caps.part_start);
+        const double fb = parts_footprint(m, n, rp, ci, br, bs);
+        *footprint = std::min(fr, fb);
+        if (fb < fr) {
+            caps.part_rows.swap(br);
+            caps.part_start.swap(bs);
+        }
+    }
+    return caps;
+}
+
 struct smfv_plan_s {
     int variant = 0, m = 0, n = 0, K = 0;
     int row_begin = 0;                     // first CSR row of the plan's row block
@@ -1490,6 +1520,9 @@ struct smfv_plan_s {
     int64_t union_rows = 0, tiled_nnz = 0, padded_nnz = 0;
     int64_t snapshot = 0;                  // values gathered by bind (tile entries + slack + direct rows)
     double reuse = 0.0, est_reuse = -1.0, analysis_ms = 0.0;
+    int ws_xcd[9] = {};            // XCD x runs tiles [ws_xcd[x], ws_xcd[x + 1])
+    int parts = 1;                 // 8: one part of the rows per XCD (build_ws_plan)
+    double footprint = -1.0;       // parts_footprint of the 8 parts
     int *tsrc = nullptr;                   // snapshot entry -> CSR index of its value (-1: pad)
     double *tvals = nullptr;               // the bound values snapshot (tile order, pads -0.0, then direct rows)
     const double *bound_values = nullptr;  // d_values the snapshot came from
@@ -1561,9 +1594,7 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
         for (int i = 0; i <= m; ++i) rpl[i] = (int)(h_rp[row_begin + i] - nnz_base);
         const int *cil = h_ci + nnz_base;
         bool go = true;
-        TileCaps caps;
-        caps.frontier = !(flags & SMFV_PLAN_NATURAL_SEEDS);
-        caps.split_ends = (flags & SMFV_PLAN_SPLIT_ENDS) ? SMFV_WS_BLOCKS_PER_XCD : 0;
+        const TileCaps caps = plan_caps(flags, row_begin, m, n, rpl.data(), cil, &p->footprint);
         if (!(flags & SMFV_PLAN_FORCE_TILES) && m > SMFV_TILE_SAMPLE_MIN_ROWS) {
             // estimate re-use on the first tiles before the full analysis
             // (which costs O(nnz * candidates))
@@ -1617,6 +1648,8 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                 rc = SMFV_ERR_INVALID;
             } else {
                 p->ntiles = W.ntiles;
+                for (int x = 0; x <= 8; ++x) p->ws_xcd[x] = W.xcd[x];
+                p->parts = caps.part_start.size() > 2 ? (int)caps.part_start.size() - 1 : 1;
                 p->union_rows = W.union_rows;
                 p->tiled_nnz = W.tiled_nnz;
                 p->padded_nnz = W.entries;
@@ -1687,9 +1720,26 @@ SMFV_API int smfv_plan_create_rows(smfv_plan_t *out, int variant, int row_begin,
 SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_col_idx,
                                double out[6])
 {
-    SMFV_REQUIRE(m >= 0 && n >= 0 && h_row_ptr && (h_row_ptr[m] == 0 || h_col_idx) && out,
+    double o[9];
+    const int rc = smfv_plan_analyse_rows(0, m, n, h_row_ptr, h_col_idx,
+                                          SMFV_PLAN_NATURAL_SEEDS | SMFV_PLAN_ONE_WAVEFRONT, o);
+    for (int i = 0; i < 6 && rc == SMFV_OK; ++i) out[i] = o[i];
+    return rc;
+}
+
+SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int *h_row_ptr_all,
+                                    const int *h_col_idx_all, int flags, double out[9])
+{
+    SMFV_REQUIRE(row_begin >= 0 && row_end >= row_begin && n >= 0 && h_row_ptr_all &&
+                     (h_row_ptr_all[row_end] == h_row_ptr_all[row_begin] || h_col_idx_all) && out,
                  "bad argument");
-    const TileCaps caps;
+    const int m = row_end - row_begin;
+    std::vector<int> rpl((size_t)m + 1);
+    for (int i = 0; i <= m; ++i) rpl[i] = h_row_ptr_all[row_begin + i] - h_row_ptr_all[row_begin];
+    const int *h_row_ptr = rpl.data();
+    const int *h_col_idx = h_col_idx_all ? h_col_idx_all + h_row_ptr_all[row_begin] : nullptr;
+    double footprint = -1.0;
+    const TileCaps caps = plan_caps(flags, row_begin, m, n, h_row_ptr, h_col_idx, &footprint);
     TileAnalysis T;
     analyse_tiles(m, n, h_row_ptr, h_col_idx, T, caps);
     // invariants of the clustered analysis the plan is built from
@@ -1729,7 +1779,7 @@ SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_
     // own caps and verified by replaying the kernel's reads
     WsPlan W;
     std::string err;
-    if (!build_ws_plan(m, n, h_row_ptr, h_col_idx, W, &err)) {
+    if (!build_ws_plan(m, n, h_row_ptr, h_col_idx, W, &err, caps)) {
         set_error("%s", err.c_str());
         return SMFV_ERR_INVALID;
     }
@@ -1739,6 +1789,24 @@ SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_
     out[3] = (double)W.direct.size();
     out[4] = (double)W.entries;
     out[5] = (double)W.tiled_nnz;
+    out[6] = caps.part_start.size() > 2 ? (double)caps.part_start.size() - 1 : 1.0;
+    out[7] = footprint;
+    // X rows the XCDs' tile ranges read, summed over the XCDs, over the
+    // block's distinct X rows (the compulsory X traffic of the XCD split)
+    std::vector<int> stamp((size_t)std::max(n, 1), -1);
+    int64_t sum = 0, total = 0;
+    for (int x = 0; x < 8; ++x)
+        for (int t = W.xcd[x]; t < W.xcd[x + 1]; ++t) {
+            const int *G = &W.grec[(size_t)t * WS_GWORDS];
+            for (int u = 0; u < G[WS_G_NU]; ++u) {
+                const int c = G[32 * ((u / 4) / 8) + 8 * (u % 4) + (u / 4) % 8];
+                if (stamp[c] != x) stamp[c] = x, ++sum;
+            }
+        }
+    std::fill(stamp.begin(), stamp.end(), -1);
+    for (int j = 0; j < h_row_ptr[m]; ++j)
+        if (stamp[h_col_idx[j]] != 0) stamp[h_col_idx[j]] = 0, ++total;
+    out[8] = total ? (double)sum / (double)total : 0.0;
     return SMFV_OK;
 }
 
@@ -1794,6 +1862,8 @@ SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS])
     out[8] = plan->analysis_ms;
     out[9] = (double)plan->snapshot;
     out[10] = plan->mfma ? 1.0 : 0.0;
+    out[11] = plan->parts;
+    out[12] = plan->footprint;
     return SMFV_OK;
 }
 
@@ -1877,7 +1947,9 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         auto kern = saddr ? (plan->fma ? k_rows_ws<0, true> : k_rows_ws<0>)
                           : (plan->fma ? k_rows_ws<0, true, false> : k_rows_ws<0, false, false>);
 #endif
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, st, plan->ntiles, K / TILE_KP, chunked,
+        WsXcd xr;
+        for (int x = 0; x <= 8; ++x) xr.first[x] = plan->ws_xcd[x];
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, st, xr, K / TILE_KP, chunked,
                            plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();
     }

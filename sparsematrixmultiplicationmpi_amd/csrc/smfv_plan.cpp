@@ -37,147 +37,179 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A, 
     int next_free = 0;
     std::vector<int> front;  // caps.frontier: unassigned neighbours of finished tiles, oldest first
     size_t fhead = 0;
-    for (int scan = 0; scan < m;) {
-        int seed = -1;
-        if (caps.frontier)
-            while (fhead < front.size() && seed < 0) {
-                const int r = front[fhead++];
-                if (!assigned[r]) seed = r;
-            }
-        if (seed < 0) {
-            while (scan < m && assigned[scan]) ++scan;
-            if (scan >= m) break;
-            seed = scan;
+    // caps.part_rows / part_start: row sets tiled one after the other (a tile
+    // takes rows of one part only); default one part of all rows in order
+    std::vector<int> own_rows, own_start;
+    const std::vector<int> *prow = &caps.part_rows, *pst = &caps.part_start;
+    if (caps.part_start.size() < 2) {
+        own_rows.resize((size_t)m);
+        for (int r = 0; r < m; ++r) own_rows[(size_t)r] = r;
+        own_start = {0, m};
+        prow = &own_rows;
+        pst = &own_start;
+    }
+    const int np = (int)pst->size() - 1;
+    std::vector<int> pid((size_t)std::max(m, 1), -1), ppos((size_t)std::max(m, 1), 0);
+    for (int x = 0; x < np; ++x)
+        for (int k = (*pst)[(size_t)x]; k < (*pst)[(size_t)x + 1]; ++k) {
+            pid[(size_t)(*prow)[(size_t)k]] = x;
+            ppos[(size_t)(*prow)[(size_t)k]] = k;
         }
-        if (caps.max_tiles > 0 && tile >= caps.max_tiles) break;
-        next_free = seed + 1;
-        int ucount = 0;
-        int64_t tnnz = 0, tpad = 0;  // real and row-padded non-zeros
-        rows.clear();
-        cand.clear();
-        const size_t ubase = A.ucols.size();
-        auto add_row = [&](int r) {
-            assigned[r] = 1;
-            rstamp[r] = tile;
-            rows.push_back(r);
-            tnnz += rp[r + 1] - rp[r];
-            tpad += (rp[r + 1] - rp[r] + caps.pad - 1) & ~(caps.pad - 1);
-            for (int j = rp[r]; j < rp[r + 1]; ++j) {
-                const int c = ci[j];
-                if (ustamp[c] != tile) {
-                    ustamp[c] = tile;
-                    upos[c] = ucount++;
-                    A.ucols.push_back(c);
+    bool stop = false;
+    for (int part = 0; part < np && !stop; ++part) {
+        const int lo = (*pst)[(size_t)part], hi = (*pst)[(size_t)part + 1];  // positions in prow
+        const int *P = prow->data();
+        A.part_tile.push_back(tile);
+        front.clear();
+        fhead = 0;
+        for (int scan = lo; scan < hi;) {
+            int seed = -1;
+            if (caps.frontier)
+                while (fhead < front.size() && seed < 0) {
+                    const int r = front[fhead++];
+                    if (!assigned[r]) seed = r;
                 }
-                if (c < m && !assigned[c] && cstamp[c] != tile) {
-                    cstamp[c] = tile;
-                    cand.push_back(c);
-                }
+            if (seed < 0) {
+                while (scan < hi && assigned[P[scan]]) ++scan;
+                if (scan >= hi) break;
+                seed = P[scan];
             }
-        };
-        add_row(seed);
-        const bool over = ucount > caps.ucap || tpad > caps.ncap;
-        while (!over && (int)rows.size() < caps.maxrows) {
-            int best = -1, best_fresh = 1 << 30;
-            long best_score = 1L << 40;
-            for (int r : cand) {
-                if (assigned[r]) continue;
-                ++probe_id;
-                int fresh = 0, inner = 0;
+            if (caps.max_tiles > 0 && tile >= caps.max_tiles) {
+                stop = true;
+                break;
+            }
+            next_free = ppos[(size_t)seed] + 1;  // position after the seed in its part
+            int ucount = 0;
+            int64_t tnnz = 0, tpad = 0;  // real and row-padded non-zeros
+            rows.clear();
+            cand.clear();
+            const size_t ubase = A.ucols.size();
+            auto add_row = [&](int r) {
+                assigned[r] = 1;
+                rstamp[r] = tile;
+                rows.push_back(r);
+                tnnz += rp[r + 1] - rp[r];
+                tpad += (rp[r + 1] - rp[r] + caps.pad - 1) & ~(caps.pad - 1);
                 for (int j = rp[r]; j < rp[r + 1]; ++j) {
                     const int c = ci[j];
-                    if (c < m && rstamp[c] == tile) ++inner;
-                    if (ustamp[c] != tile && probe[c] != probe_id) {
-                        probe[c] = probe_id;
-                        ++fresh;
+                    if (ustamp[c] != tile) {
+                        ustamp[c] = tile;
+                        upos[c] = ucount++;
+                        A.ucols.push_back(c);
+                    }
+                    const int cr = c - caps.col_base;  // the column's row in this block
+                    if (cr >= 0 && cr < m && pid[(size_t)cr] == part && !assigned[cr] && cstamp[cr] != tile) {
+                        cstamp[cr] = tile;
+                        cand.push_back(cr);
                     }
                 }
-                // fewest new union rows first; among those, the row with more
-                // neighbours already in the tile (compact blobs) and more
-                // non-zeros (re-use 5.73 -> 5.80 on the cop20k_A surrogate)
-                const int len = rp[r + 1] - rp[r];
-                const long score = (long)fresh * 64 - inner * 16 - len;
-                if (score < best_score || (score == best_score && r < best)) {
-                    best_score = score;
-                    best_fresh = fresh;
-                    best = r;
-                }
-            }
-            if (best < 0) {
-                // no neighbour left (e.g. a diagonal or block-diagonal pattern):
-                // continue with the next unassigned row in natural order
-                while (next_free < m && assigned[next_free]) ++next_free;
-                if (next_free >= m) break;
-                best = next_free;
-                ++probe_id;
-                best_fresh = 0;
-                for (int j = rp[best]; j < rp[best + 1]; ++j) {
-                    const int c = ci[j];
-                    if (ustamp[c] != tile && probe[c] != probe_id) {
-                        probe[c] = probe_id;
-                        ++best_fresh;
+            };
+            add_row(seed);
+            const bool over = ucount > caps.ucap || tpad > caps.ncap;
+            while (!over && (int)rows.size() < caps.maxrows) {
+                int best = -1, best_fresh = 1 << 30;
+                long best_score = 1L << 40;
+                for (int r : cand) {
+                    if (assigned[r]) continue;
+                    ++probe_id;
+                    int fresh = 0, inner = 0;
+                    for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                        const int c = ci[j];
+                        const int cr = c - caps.col_base;
+                        if (cr >= 0 && cr < m && rstamp[cr] == tile) ++inner;
+                        if (ustamp[c] != tile && probe[c] != probe_id) {
+                            probe[c] = probe_id;
+                            ++fresh;
+                        }
+                    }
+                    // fewest new union rows first; among those, the row with more
+                    // neighbours already in the tile (compact blobs) and more
+                    // non-zeros (re-use 5.73 -> 5.80 on the cop20k_A surrogate)
+                    const int len = rp[r + 1] - rp[r];
+                    const long score = (long)fresh * 64 - inner * 16 - len;
+                    if (score < best_score || (score == best_score && r < best)) {
+                        best_score = score;
+                        best_fresh = fresh;
+                        best = r;
                     }
                 }
+                if (best < 0) {
+                    // no neighbour left (e.g. a diagonal or block-diagonal pattern):
+                    // continue with the next unassigned row of the part
+                    while (next_free < hi && assigned[P[next_free]]) ++next_free;
+                    if (next_free >= hi) break;
+                    best = P[next_free];
+                    ++probe_id;
+                    best_fresh = 0;
+                    for (int j = rp[best]; j < rp[best + 1]; ++j) {
+                        const int c = ci[j];
+                        if (ustamp[c] != tile && probe[c] != probe_id) {
+                            probe[c] = probe_id;
+                            ++best_fresh;
+                        }
+                    }
+                }
+                if (ucount + best_fresh > caps.ucap ||
+                    tpad + ((rp[best + 1] - rp[best] + caps.pad - 1) & ~(caps.pad - 1)) > caps.ncap)
+                    break;
+                add_row(best);
             }
-            if (ucount + best_fresh > caps.ucap ||
-                tpad + ((rp[best + 1] - rp[best] + caps.pad - 1) & ~(caps.pad - 1)) > caps.ncap)
-                break;
-            add_row(best);
-        }
-        if (caps.frontier)
-            for (int r : cand)
-                if (!assigned[r]) front.push_back(r);
-        A.grow.insert(A.grow.end(), rows.begin(), rows.end());
-        // rows by decreasing length (build_ws_plan deals them to waves in
-        // this order, so the rows of a wave have similar lengths)
-        std::sort(rows.begin(), rows.end(), [&](int a, int b) {
-            const int la = rp[a + 1] - rp[a], lb = rp[b + 1] - rp[b];
-            return la != lb ? la > lb : a < b;
-        });
+            if (caps.frontier)
+                for (int r : cand)
+                    if (!assigned[r]) front.push_back(r);
+            A.grow.insert(A.grow.end(), rows.begin(), rows.end());
+            // rows by decreasing length (build_ws_plan deals them to waves in
+            // this order, so the rows of a wave have similar lengths)
+            std::sort(rows.begin(), rows.end(), [&](int a, int b) {
+                const int la = rp[a + 1] - rp[a], lb = rp[b + 1] - rp[b];
+                return la != lb ? la > lb : a < b;
+            });
 
-        TileMeta tm{};
-        tm.roff = (int)A.trows.size();
-        tm.nrows = (int)rows.size();
-        tm.noff = (int)A.padded_nnz;
-        tm.tn = (int)tnnz;
-        tm.direct = over ? 1 : 0;
-        if (over) {
-            A.ucols.resize(ubase);
-            tm.uoff = (int)ubase;
-            tm.nu = 0;
-        } else {
-            tm.uoff = (int)ubase;
-            tm.nu = ucount;
-            A.union_rows += ucount;
-            A.tiled_nnz += tnnz;
-        }
-        // tile-ordered non-zeros; every ROW segment starts at a multiple of 8
-        // entries, so the kernel's 8-wide batches of u16 / f64 LDS reads are
-        // 16-byte aligned (unaligned wide LDS reads are replayed); pads
-        // (tsrc = -1) are never summed: loops stop at the row's real length
-        int local = 0;
-        for (int r : rows) {
-            A.trows.push_back(r);
-            // packed (tile-local start, length); a direct tile's lengths are
-            // not used (the kernel reads row_ptr there)
-            const int len = rp[r + 1] - rp[r];
-            A.rbeg.push_back(over ? local : (local | (len << 16)));
-            for (int j = rp[r]; j < rp[r + 1]; ++j) {
-                A.tsrc.push_back(j);
-                A.tlidx.push_back(over ? 0 : (uint16_t)upos[ci[j]]);
-                ++local;
+            TileMeta tm{};
+            tm.roff = (int)A.trows.size();
+            tm.nrows = (int)rows.size();
+            tm.noff = (int)A.padded_nnz;
+            tm.tn = (int)tnnz;
+            tm.direct = over ? 1 : 0;
+            if (over) {
+                A.ucols.resize(ubase);
+                tm.uoff = (int)ubase;
+                tm.nu = 0;
+            } else {
+                tm.uoff = (int)ubase;
+                tm.nu = ucount;
+                A.union_rows += ucount;
+                A.tiled_nnz += tnnz;
             }
-            while (local % 8) {
-                A.tsrc.push_back(-1);
-                A.tlidx.push_back(0);
-                ++local;
+            // tile-ordered non-zeros; every ROW segment starts at a multiple of 8
+            // entries, so the kernel's 8-wide batches of u16 / f64 LDS reads are
+            // 16-byte aligned (unaligned wide LDS reads are replayed); pads
+            // (tsrc = -1) are never summed: loops stop at the row's real length
+            int local = 0;
+            for (int r : rows) {
+                A.trows.push_back(r);
+                // packed (tile-local start, length); a direct tile's lengths are
+                // not used (the kernel reads row_ptr there)
+                const int len = rp[r + 1] - rp[r];
+                A.rbeg.push_back(over ? local : (local | (len << 16)));
+                for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                    A.tsrc.push_back(j);
+                    A.tlidx.push_back(over ? 0 : (uint16_t)upos[ci[j]]);
+                    ++local;
+                }
+                while (local % 8) {
+                    A.tsrc.push_back(-1);
+                    A.tlidx.push_back(0);
+                    ++local;
+                }
             }
+            tm.tn = local;  // padded segment length (row ends come from rbeg / rp)
+            A.padded_nnz += local;
+            A.meta.push_back(tm);
+            ++tile;
         }
-        tm.tn = local;  // padded segment length (row ends come from rbeg / rp)
-        A.padded_nnz += local;
-        A.meta.push_back(tm);
-        ++tile;
     }
+    while ((int)A.part_tile.size() <= np) A.part_tile.push_back(tile);
 }
 
 // ---------------------------------------------------------------------------
@@ -244,10 +276,74 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
     }
     for (int r = 0; r < m; ++r)
         if (!seen[r]) return fail("row " + std::to_string(r) + " in no tile");
+    if (P.xcd[0] != 0 || P.xcd[8] != P.ntiles) return fail("XCD ranges do not cover the tiles");
+    for (int x = 0; x < 8; ++x)
+        if (P.xcd[x] > P.xcd[x + 1]) return fail("XCD ranges out of order");
     return true;
 }
 
 }  // namespace
+
+void range_parts(int m, const int *rp, int parts, std::vector<int> &rows, std::vector<int> &start)
+{
+    rows.resize((size_t)m);
+    for (int r = 0; r < m; ++r) rows[(size_t)r] = r;
+    start.assign((size_t)parts + 1, m);
+    start[0] = 0;
+    for (int x = 1, r = 0; x < parts; ++x) {
+        const int64_t target = (int64_t)rp[m] * x / parts;
+        while (r < m && rp[r] < target) ++r;
+        start[(size_t)x] = r;
+    }
+}
+
+void bfs_parts(int m, const int *rp, const int *ci, int col_base, int parts, std::vector<int> &rows,
+               std::vector<int> &start)
+{
+    // rows in breadth-first order from row 0 (restarting at the first
+    // unvisited row), cut into shares of equal non-zero count
+    rows.clear();
+    rows.reserve((size_t)m);
+    std::vector<char> seen((size_t)std::max(m, 1), 0);
+    for (int s = 0; s < m; ++s) {
+        if (seen[s]) continue;
+        seen[s] = 1;
+        rows.push_back(s);
+        for (size_t h = rows.size() - 1; h < rows.size(); ++h) {
+            const int r = rows[h];
+            for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                const int c = ci[j] - col_base;
+                if (c >= 0 && c < m && !seen[c]) seen[c] = 1, rows.push_back(c);
+            }
+        }
+    }
+    start.assign((size_t)parts + 1, m);
+    start[0] = 0;
+    int64_t acc = 0;
+    for (int k = 0, x = 1; k < m && x < parts; ++k) {
+        while (x < parts && acc >= (int64_t)rp[m] * x / parts) start[(size_t)x++] = k;
+        const int r = rows[(size_t)k];
+        acc += rp[r + 1] - rp[r];
+    }
+}
+
+double parts_footprint(int m, int n, const int *rp, const int *ci, const std::vector<int> &rows,
+                       const std::vector<int> &start)
+{
+    if (m <= 0 || rp[m] <= 0) return 1.0;
+    std::vector<int> stamp((size_t)std::max(n, 1), -1);
+    int64_t total = 0, sum = 0;
+    for (int j = 0; j < rp[m]; ++j)
+        if (stamp[ci[j]] != 0) stamp[ci[j]] = 0, ++total;
+    std::fill(stamp.begin(), stamp.end(), -1);
+    for (size_t x = 0; x + 1 < start.size(); ++x)
+        for (int k = start[x]; k < start[x + 1]; ++k) {
+            const int r = rows[(size_t)k];
+            for (int j = rp[r]; j < rp[r + 1]; ++j)
+                if (stamp[ci[j]] != (int)x) stamp[ci[j]] = (int)x, ++sum;
+        }
+    return (double)sum / (double)total;
+}
 
 bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::string *err, const TileCaps &caps)
 {
@@ -327,7 +423,11 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     };
     // final tiles (growth order kept for the end-halving), in wavefront order
     std::vector<std::vector<int>> tiles, stack;
-    for (const TileMeta &tm : T.meta) {
+    const int np = (int)T.part_tile.size() - 1;
+    std::vector<int> first_tile((size_t)np + 1, 0);  // final tiles: first of each part
+    for (size_t t = 0, part = 0; t < T.meta.size(); ++t) {
+        while ((int)part < np && (int)t >= T.part_tile[part + 1]) first_tile[++part] = (int)tiles.size();
+        const TileMeta &tm = T.meta[t];
         std::vector<int> rows(T.grow.begin() + tm.roff, T.grow.begin() + tm.roff + tm.nrows);
         if (tm.direct) {
             P.direct.insert(P.direct.end(), rows.begin(), rows.end());
@@ -354,9 +454,24 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
             }
         }
     }
+    for (int x = 1; x <= np; ++x)  // parts after the last tile (and empty ones) start at the end
+        if (x == np || T.part_tile[x] >= (int)T.meta.size()) first_tile[x] = std::max(first_tile[x], (int)tiles.size());
     const int nb = caps.split_ends;
     const int64_t N = (int64_t)tiles.size();
-    if (nb > 0 && N >= 8 * 3 * (int64_t)nb) {
+    // XCD x runs tiles [xcd[x], xcd[x + 1]): the 8 parts, or 8 equal shares
+    // of the order.  Each XCD's blocks run its tiles in rounds of
+    // caps.xcd_blocks; a part over the rounds every XCD needs (its first or
+    // last tiles, the part's edge) moves to the neighbouring XCD, so no block
+    // runs a round more than the tile count requires
+    for (int x = 0; x <= 8; ++x) P.xcd[x] = np == 8 ? first_tile[x] : (int)(N * x / 8);
+    if (np == 8 && N > 0) {
+        const int64_t nbk = std::max(1, caps.xcd_blocks);
+        const int64_t cap = nbk * ((N + 8 * nbk - 1) / (8 * nbk));  // tiles per XCD in the fewest rounds
+        for (int x = 1; x < 8; ++x)
+            P.xcd[x] = (int)std::max<int64_t>(std::min<int64_t>(P.xcd[x], P.xcd[x - 1] + cap),
+                                              std::max<int64_t>(N - cap * (8 - x), P.xcd[x - 1]));
+    }
+    if (nb > 0 && np == 1 && N >= 8 * 3 * (int64_t)nb) {
         // per XCD range [N x / 8, N (x + 1) / 8): its first nb tiles are cut in
         // halves; the range grows by nb, which keeps the kernel's boundaries
         // (N + 8 nb) x / 8 = N x / 8 + nb x aligned with the per-XCD rebuild
@@ -381,6 +496,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
                 if (!t.empty()) out.push_back(std::move(t));
         }
         tiles = std::move(out);
+        for (int x = 0; x <= 8; ++x) P.xcd[x] = (int)((int64_t)tiles.size() * x / 8);
     }
     for (auto &R : tiles) {
         by_length(R);

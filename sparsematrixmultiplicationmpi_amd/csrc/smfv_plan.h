@@ -66,6 +66,7 @@ struct TileAnalysis {
     int64_t union_rows = 0;        // sum of tile unions (X rows staged per panel)
     int64_t tiled_nnz = 0;         // non-zeros in non-direct tiles
     int64_t padded_nnz = 0;        // length of tsrc / tlidx
+    std::vector<int> part_tile;    // parts + 1 entries: first tile of each part, then the tile count
 };
 
 // Clustered tiling: seed a tile at the first unassigned row (or, with
@@ -87,6 +88,13 @@ struct TileCaps {
     int max_tiles = 0;             // > 0: stop after this many tiles (re-use estimate on a sample)
     bool frontier = false;         // seed each tile at the oldest unassigned neighbour of earlier tiles
     int split_ends = 0;            // build_ws_plan: > 0 = blocks per XCD whose first and last tile are halves
+    int col_base = 0;              // row block of a square pattern: column c is the block's row c - col_base
+    // row sets tiled one after the other, a tile taking rows of one set only
+    // (part x = part_rows[part_start[x] .. part_start[x + 1]), seeds scanned in
+    // that order); empty: one part, all rows in order.  build_ws_plan with 8
+    // parts runs part x on XCD x (range_parts / bfs_parts below)
+    std::vector<int> part_rows, part_start;
+    int xcd_blocks = 32;           // k_rows_ws blocks per XCD (MI355X: 256 CUs / 8 XCDs)
 };
 void analyse_tiles(int m, int n, const int *row_ptr, const int *col_idx, TileAnalysis &out,
                    const TileCaps &caps = TileCaps());
@@ -101,6 +109,7 @@ struct WsPlan {
     int64_t union_rows = 0;        // X rows staged per 32-column panel
     int64_t tiled_nnz = 0;         // non-zeros in tiles (not direct)
     int64_t entries = 0;           // used length of loff / tsrc (the vectors carry WS_SLACK more)
+    int xcd[9] = {};               // XCD x runs tiles [xcd[x], xcd[x + 1])
 };
 
 // Tiles from analyse_tiles (WS caps), each packed into the interleaved
@@ -117,6 +126,20 @@ struct WsPlan {
 // returns false (with *err) if an invariant fails.
 bool build_ws_plan(int m, int n, const int *row_ptr, const int *col_idx, WsPlan &out, std::string *err,
                    const TileCaps &caps = TileCaps());
+
+// Partitions of a block's rows into `parts` sets of equal non-zero count for
+// TileCaps::part_rows / part_start: row ranges, or shares of the rows'
+// breadth-first order from row 0 (col_base as TileCaps::col_base).
+void range_parts(int m, const int *row_ptr, int parts, std::vector<int> &rows, std::vector<int> &start);
+void bfs_parts(int m, const int *row_ptr, const int *col_idx, int col_base, int parts, std::vector<int> &rows,
+               std::vector<int> &start);
+// X rows the parts read, summed over the parts, over the block's distinct X
+// rows.  Each XCD has its own L2, so with part x on XCD x this is the
+// compulsory X traffic over X's size (1.0 = no X row read twice).  On the
+// cop20k_A surrogate: ranges 1.30, breadth-first shares 1.51, one wavefront
+// of frontier tiles cut in 8: 1.69.
+double parts_footprint(int m, int n, const int *row_ptr, const int *col_idx, const std::vector<int> &rows,
+                       const std::vector<int> &start);
 
 // ---------------------------------------------------------------------------
 // Plan of the opt-in MFMA tile kernel k_rows_mfma (SMFV_PLAN_MFMA; within

@@ -176,7 +176,8 @@ class DistPlan:
         out = (ctypes.c_double * PLAN_STATS)()
         call("smfv_dist_plan_stats", self._h, out)
         return {"tiled": bool(out[0]), "tiles": int(out[1]), "reuse": float(out[3]),
-                "row_begin": int(out[6]), "analysis_ms": float(out[8])}
+                "row_begin": int(out[6]), "analysis_ms": float(out[8]), "xcd_parts": int(out[11]),
+                "footprint": float(out[12])}
 
     def __del__(self):
         try:

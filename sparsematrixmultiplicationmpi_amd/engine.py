@@ -106,7 +106,8 @@ def _check_dense(T: torch.Tensor, rows: int, K: int, name: str) -> int:
 
 
 PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA, PLAN_NATURAL_SEEDS, PLAN_MFMA, PLAN_SPLIT_ENDS = 1, 2, 4, 8, 16, 32
-PLAN_STATS = 11  # SMFV_PLAN_STATS
+PLAN_ONE_WAVEFRONT = 64
+PLAN_STATS = 13  # SMFV_PLAN_STATS
 
 
 class SpmmPlan:
@@ -118,12 +119,15 @@ class SpmmPlan:
     tiles: "auto" (stage when re-use >= 3), "off", or "force".  fma: opt-in
     fused multiply-add in the tiled kernel (SMFV_PLAN_FMA).  rows=(begin,
     end): plan of that row block only (smfv_plan_create_rows; run() writes
-    the block's rows to Y[0:end-begin]).  The values snapshot of a tiled plan
+    the block's rows to Y[0:end-begin]).  xcd_parts: "auto" (one row range
+    per XCD when their X footprints allow it) or "one" (one wavefront cut in
+    8 shares; SMFV_PLAN_ONE_WAVEFRONT, A/B).  The values snapshot of a tiled plan
     is gathered on `stream`; a run() on another stream waits for it."""
 
     def __init__(self, variant: int, A: DeviceCSR, K: int, tiles: str = "auto", fma: bool = False,
                  stream: torch.cuda.Stream | None = None, rows: tuple[int, int] | None = None,
-                 seeds: str = "frontier", mfma: bool = False, split_ends: bool = False):
+                 seeds: str = "frontier", mfma: bool = False, split_ends: bool = False,
+                 xcd_parts: str = "auto"):
         self.variant, self.A, self.K = Variant(variant), A, K
         self.rows = rows
         flags = {"auto": 0, "off": PLAN_NO_TILES, "force": PLAN_FORCE_TILES}[tiles]
@@ -135,6 +139,8 @@ class SpmmPlan:
             flags |= PLAN_MFMA
         if split_ends:  # opt-in: half tiles first and last in every block (A/B; measured slower)
             flags |= PLAN_SPLIT_ENDS
+        if {"auto": False, "one": True}[xcd_parts]:
+            flags |= PLAN_ONE_WAVEFRONT
         self._plan = ctypes.c_void_p()
         ip = ctypes.POINTER(ctypes.c_int)
         if rows is None:
@@ -158,7 +164,8 @@ class SpmmPlan:
         return {"tiled": bool(out[0]), "tiles": int(out[1]), "staged_rows": int(out[2]),
                 "reuse": float(out[3]), "plan_bytes": int(out[4]), "direct_rows": int(out[5]),
                 "row_begin": int(out[6]), "est_reuse": float(out[7]), "analysis_ms": float(out[8]),
-                "snapshot_entries": int(out[9]), "mfma": bool(out[10])}
+                "snapshot_entries": int(out[9]), "mfma": bool(out[10]), "xcd_parts": int(out[11]),
+                "footprint": float(out[12])}
 
     def run(self, X: torch.Tensor, Y: torch.Tensor, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
         A, K = self.A, self.K

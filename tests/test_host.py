@@ -216,6 +216,48 @@ def test_tile_analysis_invariants_and_reuse():
     assert _analyse(A)[0] >= 1
 
 
+def _analyse_rows(A, r0, r1, flags=0):
+    out = (ctypes.c_double * 9)()
+    ip = ctypes.POINTER(ctypes.c_int)
+    _lib.call("smfv_plan_analyse_rows", r0, r1, A.numCols, A.rowPtr.ctypes.data_as(ip),
+              A.colIndices.ctypes.data_as(ip), flags, out)
+    return {"tiles": out[0], "reuse": out[2], "direct": out[3], "parts": int(out[6]),
+            "footprint": out[7], "xcd_footprint": out[8]}
+
+
+def test_xcd_parts_cut_compulsory_x_traffic():
+    """Each XCD has its own L2: the plan splits the rows into 8 parts (row
+    ranges or breadth-first shares, whichever reads fewer X rows) and runs
+    part x on XCD x, so the X rows the 8 XCDs read, summed, drop from 1.69x
+    to 1.30x X on the mesh-numbered surrogate (ranges) and from 2.06x to
+    1.62x on its random renumbering (breadth-first shares), at about the same
+    re-use.  The native check replays the kernel's reads of every plan."""
+    A = smfv.cop20k_surrogate()
+    m = A.numRows
+    auto = _analyse_rows(A, 0, m)
+    one = _analyse_rows(A, 0, m, 64)  # SMFV_PLAN_ONE_WAVEFRONT
+    assert auto["parts"] == 8 and one["parts"] == 1
+    assert auto["xcd_footprint"] == pytest.approx(auto["footprint"], rel=0.01)  # (a few edge tiles rebalanced)
+    assert auto["xcd_footprint"] < 1.35 < 1.6 < one["xcd_footprint"]
+    assert auto["reuse"] > 0.98 * one["reuse"] and auto["direct"] == 0
+    # no XCD runs more rounds of 32 tiles than the tile count needs
+    P = inputs.permute_symmetric(A, np.random.default_rng(7).permutation(m))
+    pa, po = _analyse_rows(P, 0, m), _analyse_rows(P, 0, m, 64)
+    assert pa["parts"] == 8 and pa["xcd_footprint"] < 1.7 < 2.0 < po["xcd_footprint"]
+    assert pa["reuse"] > 0.97 * po["reuse"]
+
+
+def test_row_block_tiles_grow_by_the_blocks_own_neighbours():
+    """A row block's tiles (one rank of the decomposition) are grown through
+    its rows' neighbours -- column c is the block's row c - row_begin -- so a
+    middle block reaches the whole matrix's re-use."""
+    A = smfv.cop20k_surrogate()
+    m = A.numRows
+    whole = _analyse_rows(A, 0, m, 64)
+    mid = _analyse_rows(A, m // 4, 3 * m // 4, 64)
+    assert mid["reuse"] > 0.97 * whole["reuse"]
+
+
 def test_mtx_reader_parallel_and_fallback(tmp_path):
     """The parallel Matrix Market parse (one entry per line, files > 64 KiB)
     gives the same CSR as the sequential token reader, and files it cannot
