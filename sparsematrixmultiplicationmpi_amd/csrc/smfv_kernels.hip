@@ -468,7 +468,8 @@ __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(
 // 4 as 2 without the per-unit barriers (waves run their units unsynchronised),
 // 5 staging and compute both running, decoupled (no barriers; compute reads
 // slot 0 while it is restaged: timing only, results are garbage), 6 as 2 with
-// half the X reads (the other half synthesised by a multiply; timing only)
+// half the X reads (the other half synthesised by a multiply; timing only),
+// 7 the full kernel without Y stores (timing only)
 // SADDR: the loaders address X, the values and the offsets by scalar base +
 // 32-bit byte offset (X and the plan's arrays each < 4 GiB; the host picks it).
 // PIPE 2 (needs SADDR): the loaders form two groups of 4 waves; group g
@@ -682,16 +683,18 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
     barrier_lds();
     int it = 0, p = 0;
     for (int u = 0; u < nunits; ++u) {
-        // (ABL >= 2 recompute the prologue's unit: slot 0 is the only staged one)
-        const char *xbase = lds + (ABL >= 2 ? 0 : (u & 1)) * XSLOT;
-        const char *mbase = lds + SL_M + (ABL >= 2 ? 0 : (it & 1)) * MSLOT;
+        // (ABL 2-6 recompute the prologue's unit: slot 0 is the only staged one)
+        constexpr bool SLOT0 = ABL >= 2 && ABL <= 6;
+        const char *xbase = lds + (SLOT0 ? 0 : (u & 1)) * XSLOT;
+        const char *mbase = lds + SL_M + (SLOT0 ? 0 : (it & 1)) * MSLOT;
         const int *R = reinterpret_cast<const int *>(mbase + M_R);
         const int row = R[slot];
         if (row >= 0 && ABL != 1) {
             const int info = R[64 + slot];
-            // the row runs nbat whole batches of 8, then (half) one of 4
-            const int js = info & 0xFFFF, nh = (info >> 16) >> 2, nbat = nh >> 1, half = nh & 1;
-            const int blast = nbat + half - 1;
+            // the row runs nbat whole batches of 8, then rem (0, 2, 4 or 6)
+            // entries of one more (its length rounded up to even)
+            const int js = info & 0xFFFF, len = info >> 16, nbat = len >> 3, rem = len & 7;
+            const int blast = nbat + (rem ? 1 : 0) - 1;
             const u4 *Lq = reinterpret_cast<const u4 *>(mbase + M_L) + js + qk;
             const d2 *Vq = reinterpret_cast<const d2 *>(mbase + M_V) + R[128 + slot] + qk;
             const char *xb0 = xbase + par * 128 + tl * 16;
@@ -731,6 +734,9 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     vn[q] = *(const volatile __attribute__((address_space(3))) d2 *)(Vq + 4 * (4 * bn + q));
+                // the first half's FP64 goes after them: it covers the offsets'
+                // latency before the next batch's X addresses need them
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     acc0 = madd(acc0, v[k], xa0[k]);
@@ -745,16 +751,32 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
                     acc1 = madd(acc1, v[4 + k], xc1[k]);
                 }
             }
-            if (half) {  // xa / vn hold the first half of batch blast: its 4 entries end the row
-                const double v[4] = {vn[0].x, vn[0].y, vn[1].x, vn[1].y};
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    acc0 = madd(acc0, v[k], xa0[k]);
-                    acc1 = madd(acc1, v[k], xa1[k]);
+            // xa / vn / ln hold the first half of batch blast: its first rem
+            // entries end the row (a wave runs a step if any of its teams needs it)
+            if (rem >= 2) {
+                acc0 = madd(acc0, vn[0].x, xa0[0]);
+                acc1 = madd(acc1, vn[0].x, xa1[0]);
+                acc0 = madd(acc0, vn[0].y, xa0[1]);
+                acc1 = madd(acc1, vn[0].y, xa1[1]);
+                if (rem >= 4) {
+                    acc0 = madd(acc0, vn[1].x, xa0[2]);
+                    acc1 = madd(acc1, vn[1].x, xa1[2]);
+                    acc0 = madd(acc0, vn[1].y, xa0[3]);
+                    acc1 = madd(acc1, vn[1].y, xa1[3]);
+                    if (rem >= 6) {
+                        rdx(ln.z, xc0[0], xc1[0], xc0[1], xc1[1]);
+                        acc0 = madd(acc0, vn[2].x, xc0[0]);
+                        acc1 = madd(acc1, vn[2].x, xc1[0]);
+                        acc0 = madd(acc0, vn[2].y, xc0[1]);
+                        acc1 = madd(acc1, vn[2].y, xc1[1]);
+                    }
                 }
             }
+            // (stored before the barrier, while the loaders wait for their
+            // DMAs: stores deferred into the next unit, among the loaders'
+            // DMA issue, measured 25.6 -> 28.1 us)
             double *y = Y + (int64_t)row * ldy + p * TILE_KP + 2 * tl;
-            if (ABL != 3 || acc0.x != acc0.x) {
+            if ((ABL != 3 && ABL != 7) || acc0.x != acc0.x) {
                 __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y + 16 * par));
                 __builtin_nontemporal_store(acc1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
             }
@@ -1940,7 +1962,8 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         if (lab_chunked >= 0) chunked = lab_chunked;
         auto kern = plan->fma ? (abl == 2 ? k_rows_ws<2, true> : k_rows_ws<0, true>)
                   : abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3>
-                  : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : abl == 6 ? k_rows_ws<6> : k_rows_ws<0>;
+                  : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : abl == 6 ? k_rows_ws<6>
+                  : abl == 7 ? k_rows_ws<7> : k_rows_ws<0>;
         if (!(saddr && lab_saddr)) kern = plan->fma ? k_rows_ws<0, true, false> : k_rows_ws<0, false, false>;
         else if (lab_pipe == 2 && abl == 0) kern = plan->fma ? k_rows_ws<0, true, true, 2> : k_rows_ws<0, false, true, 2>;
 #else

@@ -255,7 +255,7 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
             const int lb = l[64 + slot] & 0xFFFF, len = l[64 + slot] >> 16, vb = l[128 + slot];
             const int k = (slot >> 3) & 3;
             const int rl = rp[r + 1] - rp[r];
-            if (len % 4 || len < 4 || len < rl) return fail("row segment length");
+            if (len % 2 || len < rl || len > rl + 1) return fail("row segment length");
             for (int b = 0; b < (len + 7) / 8; ++b)
                 for (int u = 0; u < 8; ++u) {
                     const int el = 8 * b + u;
@@ -352,9 +352,10 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     analyse_tiles(m, n, rp, ci, T, caps);  // TileCaps defaults are the k_rows_ws caps
 
     auto len8 = [&](int r) { return std::max(8, (rp[r + 1] - rp[r] + 7) & ~7); };
-    // the length a team computes: a row ends on a whole batch of 8 or on a
-    // half batch (4); its storage stays whole batches (quad layout, len8)
-    auto len4 = [&](int r) { return std::max(4, (rp[r + 1] - rp[r] + 3) & ~3); };
+    // the length a team computes: its row's, rounded up to even (the kernel
+    // ends a row on 0, 2, 4 or 6 entries of a last batch); its storage stays
+    // whole batches (quad layout, len8)
+    auto len2 = [&](int r) { return (rp[r + 1] - rp[r] + 1) & ~1; };
     // entries of a row set sorted by decreasing length: a quad takes 4x its first (longest) row
     auto layout = [&](const std::vector<int> &rows) {
         int64_t e = 0;
@@ -390,7 +391,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
                     P.tsrc[(size_t)(noff + (int64_t)(vbase + 4 * (el / 2) + k) * 2 + el % 2)] = j;
                 }
                 lrec[slot] = r;
-                lrec[64 + slot] = lbase | (len4(r) << 16);
+                lrec[64 + slot] = lbase | (len2(r) << 16);
                 lrec[128 + slot] = vbase;
                 P.tiled_nnz += rp[r + 1] - rp[r];
             }
