@@ -472,16 +472,10 @@ __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(
 // 7 the full kernel without Y stores (timing only)
 // SADDR: the loaders address X, the values and the offsets by scalar base +
 // 32-bit byte offset (X and the plan's arrays each < 4 GiB; the host picks it).
-// PIPE 2 (needs SADDR): the loaders form two groups of 4 waves; group g
-// stages units g, g + 2, ...; per unit two barriers: P (compute finished
-// unit u: its slot is free, the group of unit u + 2 issues into it) and Q
-// (the group of unit u + 1 has drained: it landed).  A group's drain
-// overlaps the other group's issue, so the DMA stream never empties at a
-// unit boundary (PIPE 1 drains every unit before its barrier).
 struct WsXcd {
     int first[9];  // XCD x runs tiles [first[x], first[x + 1]) of the plan's order
 };
-template <int ABL, bool FMA = false, bool SADDR = true, int PIPE = 1>
+template <int ABL, bool FMA = false, bool SADDR = true>
 __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int chunked,
                                                      const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
@@ -527,69 +521,6 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
         const int wl = wv - 8;
         if (wl == 0 && lane < 32)  // zero row of both X slots
             reinterpret_cast<d2 *>(lds + (lane >> 4) * XSLOT + WS_ZOFF)[lane & 15] = d2{0.0, 0.0};
-        if constexpr (PIPE == 2) {
-            static_assert(SADDR, "the two-group pipeline uses scalar-base DMAs");
-            const int g = wl >> 2, wg = wl & 3;  // group, wave in group (16 X pieces per wave)
-            const unsigned ldxb = (unsigned)(ldx * 8);
-            i4 r0, r1, r2, r3;  // this wave's 16 union ids (record layout of 8 waves x 8 pieces)
-            int noff, tn, nu, rec_tile = -1;
-            auto tile_of = [&](int v) { return t0 + (v / npanel) * tstep; };
-            auto fetch = [&](int t) {
-                const int *G = grec + (int64_t)t * WS_GWORDS;
-                const i4 *ga = reinterpret_cast<const i4 *>(G + 32 * (2 * wg) + 8 * (lane >> 4));
-                const i4 *gb = reinterpret_cast<const i4 *>(G + 32 * (2 * wg + 1) + 8 * (lane >> 4));
-                r0 = ga[0];
-                r1 = ga[1];
-                r2 = gb[0];
-                r3 = gb[1];
-                noff = G[WS_G_NOFF + (lane & 15)];
-                tn = G[WS_G_TN + (lane & 15)];
-                nu = G[WS_G_NU + (lane & 15)];
-                rec_tile = t;
-            };
-            auto stage2 = [&](int v) {  // unit v = (tile v / npanel, panel v % npanel) into X slot v & 1
-                const int itv = v / npanel, p = v - itv * npanel, t = t0 + itv * tstep;
-                asm volatile("" ::"v"(r0), "v"(r1), "v"(r2), "v"(r3), "v"(noff), "v"(tn), "v"(nu));
-                const int uc[16] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w,
-                                    r2.x, r2.y, r2.z, r2.w, r3.x, r3.y, r3.z, r3.w};
-                const unsigned xb = lds0 + (v & 1) * XSLOT;
-                const double *xs = X + p * TILE_KP;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int piece = 16 * wg + i;  // 1 KiB = union rows 4*piece .. +3
-                    const int u = 4 * piece + (lane >> 4);
-                    if (4 * piece < nu && u < WS_UCAP)
-                        dma16s<false>(xs, (unsigned)uc[i] * ldxb + 16u * (unsigned)(lane & 15), xb + piece * 1024);
-                }
-                if (p == 0) {  // the tile's meta, once, with its first panel, into meta slot itv & 1
-                    const unsigned mb = lds0 + SL_M + (itv & 1) * MSLOT;
-                    const int nf = __builtin_amdgcn_readfirstlane(noff);
-                    for (int k = wg; k * 128 < tn; k += 4) dma16s<true>(tv + nf, 1024u * k + 16u * lane, mb + M_V + k * 1024);
-                    for (int k = wg; k * 512 < tn; k += 4)
-                        dma16s<true>(loff + nf, 1024u * k + 16u * lane, mb + M_L + k * 1024);
-                    if (wg == 3) dma16s<true>(lrec + (int64_t)t * WS_LWORDS, 16u * lane, mb + M_R);
-                }
-            };
-            // prologue: group 0 stages unit 0, group 1 unit 1; each then
-            // fetches the record of its next unit (landing with its drain)
-            if (g < nunits) {
-                fetch(tile_of(g));
-                stage2(g);
-                if (g + 2 < nunits && tile_of(g + 2) != rec_tile) fetch(tile_of(g + 2));
-            }
-            if (g == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // unit 0 landed
-            barrier_lds();                                                  // Q(-1)
-            for (int u = 0; u < nunits; ++u) {
-                barrier_lds();  // P(u): compute finished unit u, X slot u & 1 is free
-                if ((u & 1) == g && u + 2 < nunits) {
-                    stage2(u + 2);
-                    if (u + 4 < nunits && tile_of(u + 4) != rec_tile) fetch(tile_of(u + 4));
-                }
-                if (((u + 1) & 1) == g) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // unit u + 1 landed
-                barrier_lds();  // Q(u)
-            }
-            return;
-        }
         i4 u0, u1;
         int noff, tn, nu;
         unsigned xo[8];                       // SADDR: byte offset of this lane's 16 B of union row uc[i]
@@ -782,10 +713,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
             }
         }
         if (++p == npanel) p = 0, ++it;
-        if constexpr (PIPE == 2) {
-            barrier_lds();  // P(u): X slot (u & 1) is free for unit u + 2
-            barrier_lds();  // Q(u): unit u + 1 has landed
-        } else if (ABL != 4 && ABL != 5) {
+        if (ABL != 4 && ABL != 5) {
             barrier_lds();  // X slot (u & 1) is free for unit u + 2, meta slot for tile it + 1
         }
     }
@@ -1951,10 +1879,6 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             const char *e = std::getenv("SMFV_WS_SADDR");
             return !e || std::atoi(e) != 0;
         }();
-        static const int lab_pipe = [] {  // lab A/B: SMFV_WS_PIPE=2 runs the two-group loader pipeline
-            const char *e = std::getenv("SMFV_WS_PIPE");
-            return e ? std::atoi(e) : 1;
-        }();
         static const int lab_chunked = [] {  // lab A/B: SMFV_WS_CHUNKED=0/1 overrides the tile order
             const char *e = std::getenv("SMFV_WS_CHUNKED");
             return e ? std::atoi(e) : -1;
@@ -1965,7 +1889,6 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
                   : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : abl == 6 ? k_rows_ws<6>
                   : abl == 7 ? k_rows_ws<7> : k_rows_ws<0>;
         if (!(saddr && lab_saddr)) kern = plan->fma ? k_rows_ws<0, true, false> : k_rows_ws<0, false, false>;
-        else if (lab_pipe == 2 && abl == 0) kern = plan->fma ? k_rows_ws<0, true, true, 2> : k_rows_ws<0, false, true, 2>;
 #else
         auto kern = saddr ? (plan->fma ? k_rows_ws<0, true> : k_rows_ws<0>)
                           : (plan->fma ? k_rows_ws<0, true, false> : k_rows_ws<0, false, false>);
