@@ -386,7 +386,7 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
     plan = D.DistPlan(comm, smfv.Variant.ROWWISE, dA, K, to_all=True, rowpart=True, m=m)
     torch.cuda.synchronize()
     t_plan = time.time() - t0
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, 1)):  # (the first collective sets up RCCL's connections)
         plan.run(X, Y)
     torch.cuda.synchronize()
     # eager (the step holds an RCCL collective); ~65 ms per step at N = 1
@@ -494,7 +494,10 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
         torch.cuda.synchronize()
         t_plan += time.time() - t0
         copies.append((P, dX, dY))
-    for i in range(args.warmup):
+    # at least one untimed step per copy before any capture: RCCL sets up its
+    # peer connections on a communicator's first collective, which a graph
+    # capture must not contain
+    for i in range(max(args.warmup, ncopies)):
         P, dX, dY = copies[i % ncopies]
         P.run(dX, dY)
     torch.cuda.synchronize()
