@@ -458,14 +458,16 @@ def _x_rows_touched(A, r0: int, r1: int) -> int:
     return int(np.unique(np.asarray(A.colIndices[lo:hi])).size)
 
 
-def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int, variant: str) -> None:
+def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int, variant: str) -> str | None:
     """N > 1 on a matrix every rank holds (the reference's layout after its
     broadcast, SC/main.cpp:106-143): ONE problem, decomposed like the
     reference's variant (RowWise rows :26-29 / ColumnWise K columns / nnz
     ranges), each rank its share as a distributed plan (tiled where it
     pays), then the one RCCL exchange (all-gather of Y to every rank).  The
     rank-local kernel and the exchange are timed separately too, and the
-    independent-copy (replicas) rate is reported beside."""
+    independent-copy (replicas) rate is reported beside.  Returns None, or
+    the reason when no rank could build the RCCL communicator (every rank then
+    returns it, and main() runs the replicas bench with that reason attached)."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -480,7 +482,19 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     torch.cuda.set_device(dev)
     if world > 1:
         dist.init_process_group("gloo")  # control plane: barrier, max over ranks, RCCL id
-    comm = D.Communicator.from_torch_distributed()
+    try:
+        comm, err = D.Communicator.from_torch_distributed(), None
+    except Exception as e:  # e.g. RCCL refusing two ranks on one device (a 1-GPU rehearsal)
+        comm, err = None, f"{type(e).__name__}: {e}"
+    bad = torch.tensor([0.0 if comm is not None else 1.0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+    if bad.item() > 0:
+        if comm is not None:
+            comm.close()
+        if world > 1:
+            dist.destroy_process_group()
+        return err or "the RCCL communicator failed on another rank"
     X_host = inputs.generateLargeFatVector(n, K)
     prob_bytes = algorithmic_bytes(m, n, nnz, K)
     ncopies = max(1, min(16, math.ceil(args.cold_bytes / prob_bytes) + 1))
@@ -575,6 +589,7 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
         dist.destroy_process_group()
     if bad:
         sys.exit(3)
+    return None
 
 
 def main() -> None:
@@ -619,9 +634,12 @@ def main() -> None:
         bench_rowpart(args, world, rank, local, K)
         return
     mode = args.mode or ("decomposed" if world > 1 else "replicas")
+    fallback = None
     if mode == "decomposed" and kind in ("cop20k", "cop20k_perm"):
-        bench_decomposed(args, world, rank, local, kind, K, variant)
-        return
+        fallback = bench_decomposed(args, world, rank, local, kind, K, variant)
+        if fallback is None:
+            return
+        print(f"[bench] decomposed mode unavailable ({fallback}); timing replicas instead", file=sys.stderr)
 
     A, label = build_matrix(kind, args.mtx)
     m, n, nnz = A.numRows, A.numCols, A.nnz
@@ -799,6 +817,9 @@ def main() -> None:
             "cpu_baseline": cpu,
             "vendor_rocsparse": vendor,
         }
+        if fallback is not None:
+            out["decomposed_fallback"] = {"reason": fallback,
+                                          "note": "the decomposed (RCCL) mode could not start; these are replicas"}
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
