@@ -90,7 +90,7 @@ def measured_traffic(config: str, kernel: str):
 
 
 def kernel_label(variant: str, K: int, plan_stats: dict, x_bytes: int = 0) -> str:
-    if variant == "NONZERO":
+    if variant == "NONZERO" and not plan_stats.get("tiled"):
         return "k_merge_flat + k_carry_fixup" if K % 32 == 0 else "k_merge + k_carry_fixup"
     if plan_stats.get("mfma"):
         return "k_rows_mfma"

@@ -103,7 +103,7 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz,
 
 /* ---- plans: analysed once per (matrix pattern, K), executed many times --
  * The plan owns all device workspace (merge-path carries for NONZERO) and,
- * for SEQUENTIAL / ROWWISE / COLUMNWISE with K a multiple of 32, a clustered
+ * with K a multiple of 32, a clustered
  * row-tile analysis of the pattern (h_col_idx needed): tiles of <= 64 rows
  * grown by adjacency whose distinct X rows (<= 239) fit a 60 KiB LDS image,
  * with a tile-ordered copy of the values and 16-bit X-row offsets.  The tiled
@@ -113,7 +113,10 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz,
  * gathered straight from X by a second launch.  Tiling is used when the
  * re-use (non-zeros per staged X row) is >= 3 -- estimated first on 512 tiles
  * grown in the full pattern, so the decision does not depend on the row
- * numbering -- or when SMFV_PLAN_FORCE_TILES is set.
+ * numbering -- or when SMFV_PLAN_FORCE_TILES is set.  A NONZERO plan over
+ * whole rows takes the same tiled kernel under the same rule (bit-identical
+ * to the reference's NonZeroElement with one rank, which sums every row in
+ * CSR order); otherwise, and with SMFV_PLAN_NO_TILES, it runs the merge path.
  *
  * Values contract of a TILED plan: smfv_plan_bind_values gathers a snapshot
  * of A's device values (tile order, and the directly-gathered rows) and the

@@ -1534,12 +1534,23 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
     };
     fail_hip(hipEventCreateWithFlags(&p->bind_ev, hipEventDisableTiming), "hipEventCreate");
     if (variant == SMFV_NONZERO) {
+        // the merge-path workspace (the untiled path, and inputs the tiled
+        // kernel cannot take: unaligned X / Y)
         p->ws_bytes = merge_workspace_bytes(m, p->nnz, K);
         if (p->ws_bytes) {
             fail_hip(hipMalloc(&p->ws, p->ws_bytes), "hipMalloc(workspace)");
             p->dev_bytes += p->ws_bytes;
         }
-    } else if (!rc && h_rp && h_ci && m > 0 && K > 0 && K % TILE_KP == 0 && !(flags & SMFV_PLAN_NO_TILES)) {
+    }
+    // NONZERO on whole rows (one device: the reference's NonZeroElement with
+    // one rank sums every row in CSR order, SC/...NonZeroElement.cpp:56-67)
+    // takes the tiled row kernel when the pattern has the re-use for it --
+    // bit-identical to that; skewed or re-use-free patterns (config 4), nnz
+    // ranges that cut rows (a rank's share) and SMFV_PLAN_NO_TILES keep the
+    // nnz-balanced merge path
+    const bool whole_rows = variant != SMFV_NONZERO ||
+                            (h_rp && h_rp[row_begin] == nnz_base && h_rp[row_begin + m] == nnz_end);
+    if (!rc && whole_rows && h_rp && h_ci && m > 0 && K > 0 && K % TILE_KP == 0 && !(flags & SMFV_PLAN_NO_TILES)) {
         std::vector<int> rpl((size_t)m + 1);
         for (int i = 0; i <= m; ++i) rpl[i] = (int)(h_rp[row_begin + i] - nnz_base);
         const int *cil = h_ci + nnz_base;

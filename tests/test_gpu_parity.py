@@ -2,7 +2,8 @@
 
 Bit-exact: SEQUENTIAL / ROWWISE / COLUMNWISE against the reference's own
 outputs (golden fixtures) and against the oracle on larger inputs.
-NONZERO (merge-path): deterministic, within 1e-12 of the sequential result
+NONZERO (merge-path; on one device with X-row re-use the tiled row kernel,
+bit-identical): deterministic, within 1e-12 of the sequential result
 relative to sum|a||x| (tolerance written here; the north star allows 1e-6
 relative, the reference's own check is 1e-6 absolute, SC/utils.cpp:55).
 """
@@ -147,6 +148,35 @@ def test_cop20k_surrogate_full_size(gpu):
         assert np.array_equal(bits(Y), bits(Yref)), K
         # the reference's own acceptance check (absolute 1e-6, SC/utils.cpp:55)
         assert smfv.areMatricesEqual(run(smfv.Variant.NONZERO, A, X, gpu), Yref, 1e-6)
+
+
+def test_nonzero_one_device_plan_choice(gpu):
+    """NONZERO on one device: on a pattern with X-row re-use the plan takes
+    the tiled row kernel and equals the sequential sum bit for bit -- what the
+    reference's NonZeroElement computes with one rank (its single nnz range
+    sums every row in CSR order, SC/...NonZeroElement.cpp:56-67); tiles="off"
+    keeps the nnz-balanced merge path (within 1e-12 of sum|a||x|, deterministic);
+    a re-use-free power-law pattern stays on the merge path."""
+    A = smfv.cop20k_surrogate()
+    K = 32
+    X = smfv.generateLargeFatVector(A.numCols, K)
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    absY = oracle.spmm("sequential", A.rowPtr, A.colIndices, np.abs(A.values), np.abs(X))
+    dA = smfv.DeviceCSR(A, gpu)
+    dX = torch.from_numpy(X).to(gpu)
+    tiled = smfv.SpmmPlan(smfv.Variant.NONZERO, dA, K)
+    merge = smfv.SpmmPlan(smfv.Variant.NONZERO, dA, K, tiles="off")
+    assert tiled.stats()["tiled"] and not merge.stats()["tiled"]
+    outs = []
+    for plan in (tiled, merge, merge):
+        Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+        plan.run(dX, Y)
+        torch.cuda.synchronize()
+        outs.append(Y.cpu().numpy())
+    assert np.array_equal(bits(outs[0]), bits(Yref))
+    assert rel_err(outs[1], Yref, absY) <= NNZ_TOL and np.array_equal(bits(outs[1]), bits(outs[2]))
+    B = smfv.gen_random_rows(60000, 50000, 16, 2.0, 4096, 3)
+    assert not smfv.SpmmPlan(smfv.Variant.NONZERO, smfv.DeviceCSR(B, gpu), K).stats()["tiled"]
 
 
 def test_rank_local_building_blocks(gpu):
