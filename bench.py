@@ -316,6 +316,8 @@ def _graph_or_eager(step, steps: int, world: int):
     (RCCL calls included) when capture works, else launched eagerly.
     Returns (ms per step, how)."""
     import torch
+    import torch.distributed as dist
+    g, err = None, None
     try:
         g = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream()
@@ -325,19 +327,27 @@ def _graph_or_eager(step, steps: int, world: int):
                 for i in range(steps):
                     step(i)
         torch.cuda.current_stream().wait_stream(side)
+    except Exception as e:  # capture refused (e.g. a collective that cannot be captured)
+        g, err = None, e
+    torch.cuda.synchronize()
+    if world > 1:  # every rank replays, or none does (the graph holds collectives)
+        ok = torch.tensor([0.0 if g is None else 1.0], dtype=torch.float64)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if ok.item() == 0.0:
+            g = None
+    if g is not None:
         g.replay()
         torch.cuda.synchronize()
         return _timed_events(g.replay, world) / steps, "hipGraph replay"
-    except Exception as e:  # capture refused (e.g. a collective that cannot be captured)
-        torch.cuda.synchronize()
-        print(f"[bench] graph capture failed ({e!r:.120}); timing eager launches", file=sys.stderr)
-        for i in range(3):
-            step(i)
+    print(f"[bench] graph capture failed here or on another rank ({err!r:.120}); timing eager launches",
+          file=sys.stderr)
+    for i in range(3):
+        step(i)
 
-        def run():
-            for i in range(steps):
-                step(i)
-        return _timed_events(run, world) / steps, "eager launches"
+    def run():
+        for i in range(steps):
+            step(i)
+    return _timed_events(run, world) / steps, "eager launches"
 
 
 def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
@@ -489,11 +499,9 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     bad = torch.tensor([0.0 if comm is not None else 1.0], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(bad, op=dist.ReduceOp.MAX)
-    if bad.item() > 0:
+    if bad.item() > 0:  # (the gloo group stays up for main's replicas bench)
         if comm is not None:
             comm.close()
-        if world > 1:
-            dist.destroy_process_group()
         return err or "the RCCL communicator failed on another rank"
     X_host = inputs.generateLargeFatVector(n, K)
     prob_bytes = algorithmic_bytes(m, n, nnz, K)
@@ -665,9 +673,10 @@ def main() -> None:
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
-    if world > 1:
+    if world > 1 and not dist.is_initialized():
         # --mode replicas: control plane only (barrier + max over ranks), every
-        # rank runs its own copy of the problem
+        # rank runs its own copy of the problem (a decomposed-mode fallback
+        # arrives with the group already up)
         dist.init_process_group("gloo")
 
     # ---- resident problem copies ----------------------------------------
