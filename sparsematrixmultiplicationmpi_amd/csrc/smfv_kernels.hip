@@ -657,30 +657,36 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
                 rdx(ln.z, xc0[0], xc1[0], xc0[1], xc1[1]);  // second half of batch b
                 rdx(ln.w, xc0[2], xc1[2], xc0[3], xc1[3]);
                 __builtin_amdgcn_sched_barrier(0);
-                const double v[8] = {vn[0].x, vn[0].y, vn[1].x, vn[1].y, vn[2].x, vn[2].y, vn[3].x, vn[3].y};
-                // next batch's meta (the last batch re-reads itself); volatile
-                // keeps these reads here, behind this batch's X reads
+                // next batch's offsets (the last batch re-reads itself); volatile
+                // keeps the read here, behind this batch's X reads
                 const int bn = min(b + 1, blast);
                 ln = *(const volatile __attribute__((address_space(3))) u4 *)(Lq + 4 * bn);
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    vn[q] = *(const volatile __attribute__((address_space(3))) d2 *)(Vq + 4 * (4 * bn + q));
-                // the first half's FP64 goes after them: it covers the offsets'
+                // the first half's FP64 goes after it: it covers the offsets'
                 // latency before the next batch's X addresses need them
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    acc0 = madd(acc0, v[k], xa0[k]);
-                    acc1 = madd(acc1, v[k], xa1[k]);
+                    acc0 = madd(acc0, (k & 1) ? vn[k >> 1].y : vn[k >> 1].x, xa0[k]);
+                    acc1 = madd(acc1, (k & 1) ? vn[k >> 1].y : vn[k >> 1].x, xa1[k]);
                 }
+                __builtin_amdgcn_sched_barrier(0);
+                // each value pair is re-read in place once its FP64 has issued
+                // (no register copies of the batch's values)
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    vn[q] = *(const volatile __attribute__((address_space(3))) d2 *)(Vq + 4 * (4 * bn + q));
                 rdx(ln.x, xa0[0], xa1[0], xa0[1], xa1[1]);  // first half of batch b + 1
                 rdx(ln.y, xa0[2], xa1[2], xa0[3], xa1[3]);
                 __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the second half's FP64
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    acc0 = madd(acc0, v[4 + k], xc0[k]);
-                    acc1 = madd(acc1, v[4 + k], xc1[k]);
+                    acc0 = madd(acc0, (k & 1) ? vn[2 + (k >> 1)].y : vn[2 + (k >> 1)].x, xc0[k]);
+                    acc1 = madd(acc1, (k & 1) ? vn[2 + (k >> 1)].y : vn[2 + (k >> 1)].x, xc1[k]);
                 }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 2; q < 4; ++q)
+                    vn[q] = *(const volatile __attribute__((address_space(3))) d2 *)(Vq + 4 * (4 * bn + q));
             }
             // xa / vn / ln hold the first half of batch blast: its first rem
             // entries end the row (a wave runs a step if any of its teams needs it)
