@@ -475,6 +475,25 @@ __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(
 struct WsXcd {
     int first[9];  // XCD x runs tiles [first[x], first[x + 1]) of the plan's order
 };
+#ifdef SMFV_LAB
+// lab ABL 8: per (block, wave, unit) two s_memtime stamps -- compute waves:
+// unit start (after its barrier), rows stored; loader waves: the next unit's
+// DMAs issued, landed (vmcnt 0) -- written by lane 0 with vector stores
+__device__ unsigned long long *ws_stamps = nullptr;
+constexpr int WS_STAMP_UNITS = 32;
+#define WS_STAMP(ABL_, u_, k_)                                                                                    \
+    do {                                                                                                          \
+        if constexpr (ABL_ == 8)                                                                                  \
+            if (lane == 0 && (u_) < WS_STAMP_UNITS)                                                               \
+                ((__attribute__((address_space(1))) unsigned long long *)ws_stamps)                               \
+                    [(((size_t)blockIdx.x * 16 + wv) * WS_STAMP_UNITS + (u_)) * 2 + (k_)] =                       \
+                        __builtin_amdgcn_s_memtime(); /* global (vector) store: not counted by lgkmcnt */         \
+    } while (0)
+#else
+#define WS_STAMP(ABL_, u_, k_) \
+    do {                       \
+    } while (0)
+#endif
 template <int ABL, bool FMA = false, bool SADDR = true>
 __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int chunked,
                                                      const int *__restrict__ grec,
@@ -594,7 +613,9 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
                 if (p == npanel - 1) fetch_record(min(t + tstep, tlast));
                 if (++p == npanel) p = 0, ++it;
             }
+            WS_STAMP(ABL, u, 0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // unit u+1 has landed
+            WS_STAMP(ABL, u, 1);
             if (ABL != 4 && ABL != 5) barrier_lds();
         }
         return;
@@ -618,6 +639,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
         constexpr bool SLOT0 = ABL >= 2 && ABL <= 6;
         const char *xbase = lds + (SLOT0 ? 0 : (u & 1)) * XSLOT;
         const char *mbase = lds + SL_M + (SLOT0 ? 0 : (it & 1)) * MSLOT;
+        WS_STAMP(ABL, u, 0);
         const int *R = reinterpret_cast<const int *>(mbase + M_R);
         const int row = R[slot];
         if (row >= 0 && ABL != 1) {
@@ -718,6 +740,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
                 __builtin_nontemporal_store(acc1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
             }
         }
+        WS_STAMP(ABL, u, 1);
         if (++p == npanel) p = 0, ++it;
         if (ABL != 4 && ABL != 5) {
             barrier_lds();  // X slot (u & 1) is free for unit u + 2, meta slot for tile it + 1
@@ -1904,8 +1927,16 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         auto kern = plan->fma ? (abl == 2 ? k_rows_ws<2, true> : k_rows_ws<0, true>)
                   : abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3>
                   : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : abl == 6 ? k_rows_ws<6>
-                  : abl == 7 ? k_rows_ws<7> : k_rows_ws<0>;
+                  : abl == 7 ? k_rows_ws<7> : abl == 8 ? k_rows_ws<8> : k_rows_ws<0>;
         if (!(saddr && lab_saddr)) kern = plan->fma ? k_rows_ws<0, true, false> : k_rows_ws<0, false, false>;
+        static unsigned long long *stamp_buf = nullptr;
+        const size_t stamp_n = (size_t)blocks * 16 * WS_STAMP_UNITS * 2;
+        if (abl == 8 && !stamp_buf) {
+            SMFV_HIP(hipMalloc(reinterpret_cast<void **>(&stamp_buf), 256 * 16 * WS_STAMP_UNITS * 2 * 8));
+            SMFV_HIP(hipMemcpyToSymbol(HIP_SYMBOL(ws_stamps), &stamp_buf, sizeof(stamp_buf)));
+        }
+        SMFV_REQUIRE(abl != 8 || blocks <= 256, "lab stamps: at most 256 blocks");
+        if (abl == 8) SMFV_HIP(hipMemsetAsync(stamp_buf, 0, stamp_n * 8, st));
 #else
         auto kern = saddr ? (plan->fma ? k_rows_ws<0, true> : k_rows_ws<0>)
                           : (plan->fma ? k_rows_ws<0, true, false> : k_rows_ws<0, false, false>);
@@ -1915,6 +1946,18 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, st, xr, K / TILE_KP, chunked,
                            plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();
+#ifdef SMFV_LAB
+        if (abl == 8)
+            if (const char *path = std::getenv("SMFV_WS_STAMPS")) {  // eager runs only: dump this launch's stamps
+                std::vector<unsigned long long> h(stamp_n);
+                SMFV_HIP(hipStreamSynchronize(st));
+                SMFV_HIP(hipMemcpy(h.data(), stamp_buf, stamp_n * 8, hipMemcpyDeviceToHost));
+                if (FILE *f = std::fopen(path, "wb")) {
+                    std::fwrite(h.data(), 8, h.size(), f);
+                    std::fclose(f);
+                }
+            }
+#endif
     }
     if (plan->ndirect > 0) {
         hipLaunchKernelGGL(k_rows_list, dim3((unsigned)((plan->ndirect + 31) / 32), (unsigned)(K / TILE_KP)),
