@@ -57,6 +57,8 @@ def metric_for(config: str, K: int, variant: str) -> str:
     what = {"cop20k": "cop20k_A", "pow10m": "synthetic 10M x 10M power-law", "syn80m": "synthetic 80M x 80M",
             "cop20k_perm": "cop20k_A (randomly permuted)"}[CONFIGS[config][0]]
     return f"effective GFLOP/s + achieved HBM GB/s, {what} × K={K}, {variant}"
+
+
 STABILIZE_REPLAYS_COLLECTIVE = 10  # the same, as a count every rank replays (graphs with RCCL calls)
 STABILIZE_S = 0.1  # untimed graph replays before the first timed region (clock ramp)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -494,8 +496,9 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     pays), then the one RCCL exchange (all-gather of Y to every rank).  The
     rank-local kernel and the exchange are timed separately too, and the
     independent-copy (replicas) rate is reported beside.  Returns None, or
-    the reason when no rank could build the RCCL communicator (every rank then
-    returns it, and main() runs the replicas bench with that reason attached)."""
+    the reason when any rank could not build the RCCL communicator (the
+    ranks agree over gloo; every rank then returns, and main() runs the
+    replicas bench with that reason attached)."""
     import numpy as np
     import torch
     import torch.distributed as dist
