@@ -346,3 +346,61 @@ def test_exchange_schedule_delivers_every_block(p, variant, mode):
     targets = range(p) if mode == 1 else [root]
     for t in targets:
         assert owners <= have[t], (t, owners - have[t])
+
+
+def _both_readers(path):
+    A = smfv.readMatrixMarketFile(str(path))
+    m, n, rp, ci, va = oracle.mtx_read(str(path))
+    assert (A.numRows, A.numCols) == (m, n)
+    assert np.array_equal(A.rowPtr, rp) and np.array_equal(A.colIndices, ci) and np.array_equal(A.values, va)
+    return A
+
+
+def test_mtx_reader_reference_quirks(tmp_path):
+    """Known answers for what SC/utils.cpp:70-185 does beyond the Matrix
+    Market spec, on the product reader and the oracle alike: the
+    symmetric / pattern flags come from ANY comment line containing the word
+    (:84-105), so "skew-symmetric" mirrors like "symmetric" and its mirror is
+    NOT negated (:149-152); duplicates stay, and std::sort on (col, value)
+    pairs orders a row's duplicates by value (:157-160); an "integer" field is
+    read as a double; entries past the header's count are ignored (:124)."""
+    p = tmp_path / "skew.mtx"
+    p.write_text("%%MatrixMarket matrix coordinate real skew-symmetric\n3 3 2\n2 1 -4.5\n3 2 2.0\n")
+    A = _both_readers(p)
+    assert A.rowPtr.tolist() == [0, 1, 3, 4]
+    assert A.colIndices.tolist() == [1, 0, 2, 1]
+    assert A.values.tolist() == [-4.5, -4.5, 2.0, 2.0]  # mirrored, not negated
+    p = tmp_path / "later.mtx"  # the flag words in a later comment line count
+    p.write_text("%%MatrixMarket matrix coordinate real general\n% not symmetric, no pattern\n2 2 1\n2 1\n")
+    A = _both_readers(p)
+    assert A.rowPtr.tolist() == [0, 1, 2] and A.colIndices.tolist() == [1, 0] and A.values.tolist() == [1.0, 1.0]
+    p = tmp_path / "dups.mtx"  # duplicates ordered by value; integer field
+    p.write_text("%%MatrixMarket matrix coordinate integer general\n2 3 5\n1 2 7\n1 2 -3\n1 1 9\n2 3 1\n1 2 5\n"
+                 "2 2 99\n")
+    A = _both_readers(p)
+    assert A.rowPtr.tolist() == [0, 4, 5]
+    assert A.colIndices.tolist() == [0, 1, 1, 1, 2]
+    assert A.values.tolist() == [9.0, -3.0, 5.0, 7.0, 1.0]  # the sixth entry (2 2 99) is past the count
+
+
+def test_mtx_reader_reference_quirks_parallel_parse(tmp_path):
+    """The same quirks through the parallel parse (files over 64 KiB): a
+    skew-symmetric banner, an integer field, duplicates with distinct
+    values, against the oracle's sequential restatement."""
+    rng = np.random.default_rng(5)
+    m = 3000
+    r = rng.integers(1, m + 1, 20000)
+    c = rng.integers(1, m + 1, 20000)
+    keep = r >= c  # lower triangle, as a symmetric file stores it
+    r, c = r[keep], c[keep]
+    r = np.concatenate([r, r[:500]])  # duplicates of the first 500 entries, other values
+    c = np.concatenate([c, c[:500]])
+    v = rng.integers(-50, 50, r.size)
+    p = tmp_path / "big_skew.mtx"
+    with open(p, "w") as f:
+        f.write("%%MatrixMarket matrix coordinate integer skew-symmetric\n%\n")
+        f.write(f"{m} {m} {r.size}\n")
+        f.writelines(f"{a} {b} {x}\n" for a, b, x in zip(r, c, v))
+    assert p.stat().st_size > 64 * 1024
+    A = _both_readers(p)
+    assert A.nnz == 2 * r.size - int(np.sum(r == c))
