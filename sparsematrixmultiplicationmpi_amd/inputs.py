@@ -114,7 +114,11 @@ def deserialize(flat: np.ndarray, rows: int, cols: int) -> np.ndarray:
 
 
 def areMatricesEqual(mat1, mat2, tolerance: float) -> bool:
-    """SC/utils.cpp:38-63: same shape and max |a-b| <= tolerance (absolute)."""
+    """SC/utils.cpp:38-63: same shape and max |a-b| <= tolerance (absolute).
+    One deliberate difference: a NaN difference counts as unequal here (and in
+    the device compare, smfv_compare_f64), where the reference's
+    `fabs(a - b) > tolerance` is false for NaN and calls the matrices equal;
+    the C++ drop-in's areMatricesEqual keeps the reference's behaviour."""
     a, b = np.asarray(mat1, dtype=np.float64), np.asarray(mat2, dtype=np.float64)
     if a.shape != b.shape:
         return False

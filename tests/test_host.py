@@ -404,3 +404,11 @@ def test_mtx_reader_reference_quirks_parallel_parse(tmp_path):
     assert p.stat().st_size > 64 * 1024
     A = _both_readers(p)
     assert A.nnz == 2 * r.size - int(np.sum(r == c))
+
+
+def test_are_matrices_equal_nan_policy():
+    """The Python mirror (and the device compare) treat a NaN difference as
+    unequal; the reference's fabs(NaN) > tol is false (SC/utils.cpp:55), which
+    the C++ drop-in keeps -- documented in inputs.areMatricesEqual."""
+    assert not smfv.areMatricesEqual([[1.0, float("nan")]], [[1.0, 2.0]], 1e-6)
+    assert smfv.areMatricesEqual([[1.0, 2.0]], [[1.0, 2.0 + 5e-7]], 1e-6)
