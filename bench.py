@@ -312,6 +312,45 @@ def sampled_check(A, rows, dX, Ydev, exact: bool, row_base: int = 0) -> dict:
             "seconds": round(time.time() - t0, 1)}
 
 
+class Deadline:
+    """Per-phase watchdog for the multi-GPU paths: if a phase (communicator
+    set-up, plan creation, warm-up, timing, check) runs past its limit -- an
+    RCCL call that never returns on a first 8-GPU run -- the watchdog prints
+    one diagnostic JSON line naming the phase and ends the process with exit
+    status 4, so the driver gets a line and a status instead of a timeout.
+    A ctypes / HIP call releases the GIL, so the watchdog thread runs while
+    the main thread is stuck in one."""
+
+    def __init__(self, seconds: float, rank: int, world: int, metric: str):
+        self.seconds, self.rank, self.world, self.metric = seconds, rank, world, metric
+        self.timer = None
+        self.phase = None
+
+    def enter(self, phase: str) -> None:
+        import threading
+        self.cancel()
+        self.phase = phase
+        if self.seconds <= 0:
+            return
+        t0 = time.time()
+
+        def expire():
+            print(json.dumps({"metric": self.metric, "value": None, "unit": "GFLOP/s", "n_gpus": self.world,
+                              "error": f"rank {self.rank}: phase '{phase}' exceeded its {self.seconds:.0f} s "
+                                       f"deadline ({time.time() - t0:.0f} s)", "rank": self.rank}), flush=True)
+            print(f"[bench] rank {self.rank}: deadline in phase {phase}; exiting with status 4",
+                  file=sys.stderr, flush=True)
+            os._exit(4)
+        self.timer = threading.Timer(self.seconds, expire)
+        self.timer.daemon = True
+        self.timer.start()
+
+    def cancel(self) -> None:
+        if self.timer is not None:
+            self.timer.cancel()
+            self.timer = None
+
+
 def _timed_events(fn, world: int):
     """HIP events on the current stream around fn(), bracketed by a barrier +
     synchronize on both sides (max over ranks is taken by the caller)."""
@@ -389,6 +428,7 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
     from sparsematrixmultiplicationmpi_amd import inputs, sampling
 
     m = n = args.rows or SYN80M_ROWS
+    dl = Deadline(args.phase_timeout, rank, world, metric_for("syn80m_k32", K, "ROWWISE"))
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # before the GPU is touched; the reference's int32 m*K indexing cannot
@@ -405,9 +445,11 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
+    dl.enter("process group + RCCL communicator")
     if world > 1:
         dist.init_process_group("gloo")
     comm = D.Communicator.from_torch_distributed()
+    dl.enter("inputs + plan")
     dA = smfv.DeviceCSR(A, dev)
     X = torch.empty((n, K), dtype=torch.float64, device=dev)
     smfv.fill_x_hash(X, 43)
@@ -416,13 +458,22 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
     plan = D.DistPlan(comm, smfv.Variant.ROWWISE, dA, K, to_all=True, rowpart=True, m=m)
     torch.cuda.synchronize()
     t_plan = time.time() - t0
+    dl.enter("warm-up (first collective: RCCL connection set-up)")
     for _ in range(max(args.warmup, 1)):  # (the first collective sets up RCCL's connections)
         plan.run(X, Y)
     torch.cuda.synchronize()
     # eager (the step holds an RCCL collective); ~65 ms per step at N = 1
+    dl.enter("timed steps")
     ms_step = _timed_events(lambda: [plan.run(X, Y) for _ in range(args.steps)], world) / args.steps
     ms_kern = _timed_events(lambda: [plan.run_local(X, Y) for _ in range(args.steps)], world) / args.steps
+    # the reference's own exchange semantics beside it: Gatherv to rank 0
+    # (SC/...RowWise.cpp:85-87) instead of the all-gather
+    plan_root = D.DistPlan(comm, smfv.Variant.ROWWISE, dA, K, to_all=False, rowpart=True, m=m)
+    plan_root.run(X, Y)
+    ms_root = _timed_events(lambda: [plan_root.run(X, Y) for _ in range(args.steps)], world) / args.steps
+    del plan_root
     # sampled check, outside the timed region: rank 0's rows + rows of the other blocks
+    dl.enter("result check")
     plan.run(X, Y)
     torch.cuda.synchronize()
     chk = None
@@ -437,7 +488,7 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
                 other_ok &= c["ok"]
                 other_n += 1
         chk["other_blocks_rows_checked"], chk["ok"] = other_n, chk["ok"] and other_ok
-    t = torch.tensor([ms_step, ms_kern, float(nnz_loc)], dtype=torch.float64)
+    t = torch.tensor([ms_step, ms_kern, float(nnz_loc), ms_root], dtype=torch.float64)
     if world > 1:
         tn = torch.tensor([float(nnz_loc)], dtype=torch.float64)
         dist.all_reduce(tn)
@@ -445,7 +496,8 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
         nnz_tot = int(tn.item())
     else:
         nnz_tot = nnz_loc
-    ms_step, ms_kern = float(t[0]), float(t[1])
+    dl.cancel()
+    ms_step, ms_kern, ms_root = float(t[0]), float(t[1]), float(t[3])
     mloc = r1 - r0
     flops = 2.0 * nnz_tot * K
     kbytes = 12 * nnz_loc + 4 * (mloc + 1) + 8 * n * K + 8 * mloc * K  # rank 0's block, X read once
@@ -469,6 +521,11 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
                          "avg_launch_ms": round(ms_kern, 4),
                          "timing": "HIP events around eager launches (rank-local kernel alone; max over ranks)"},
             "exchange_ms": round(ms_step - ms_kern, 4),
+            "exchange_ms_gather_to_root": round(ms_root - ms_kern, 4),
+            "exchange_note": "exchange_ms: all-gather of the Y blocks to every rank (ncclAllGather); "
+                             "exchange_ms_gather_to_root: the reference's MPI_Gatherv semantics (grouped "
+                             "ncclSend/ncclRecv to rank 0, SC/...RowWise.cpp:85-87); each = (kernel + "
+                             "exchange) - kernel alone, max over ranks",
             "host_generation_s": round(t_gen, 1), "plan_create_s": round(t_plan, 2),
             "check": chk,
             "cpu_baseline": cpu,
@@ -508,9 +565,11 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
 
     A, label = build_matrix(kind, args.mtx)
     m, n, nnz = A.numRows, A.numCols, A.nnz
+    dl = Deadline(args.phase_timeout, rank, world, metric_for(args.config, K, variant))
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
+    dl.enter("process group + RCCL communicator")
     if world > 1:
         dist.init_process_group("gloo")  # control plane: barrier, max over ranks, RCCL id
     try:
@@ -521,9 +580,11 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     if world > 1:
         dist.all_reduce(bad, op=dist.ReduceOp.MAX)
     if bad.item() > 0:  # (the gloo group stays up for main's replicas bench)
+        dl.cancel()
         if comm is not None:
             comm.close()
         return err or "the RCCL communicator failed on another rank"
+    dl.enter("inputs + distributed plans")
     X_host = inputs.generateLargeFatVector(n, K)
     prob_bytes = algorithmic_bytes(m, n, nnz, K)
     ncopies = max(1, min(16, math.ceil(args.cold_bytes / prob_bytes) + 1))
@@ -534,33 +595,44 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
         dY = torch.zeros((m, K), dtype=torch.float64, device=dev)
         t0 = time.time()
         P = D.DistPlan(comm, smfv.Variant[variant], dA, K, to_all=True, tiles=args.tiles)
+        # the same share with the reference's exchange semantics: gather to
+        # rank 0 only (MPI_Gatherv / MPI_Reduce to the root)
+        Pr = D.DistPlan(comm, smfv.Variant[variant], dA, K, to_all=False, tiles=args.tiles)
         torch.cuda.synchronize()
         t_plan += time.time() - t0
-        copies.append((P, dX, dY))
+        copies.append((P, dX, dY, Pr))
     # at least one untimed step per copy before any capture: RCCL sets up its
     # peer connections on a communicator's first collective, which a graph
     # capture must not contain
+    dl.enter("warm-up (first collectives: RCCL connection set-up)")
     for i in range(max(args.warmup, ncopies)):
-        P, dX, dY = copies[i % ncopies]
+        P, dX, dY, Pr = copies[i % ncopies]
         P.run(dX, dY)
+        Pr.run(dX, dY)
     torch.cuda.synchronize()
+    dl.enter("timed steps")
     ms_step, how = _graph_or_eager(lambda i: copies[i % ncopies][0].run(copies[i % ncopies][1],
                                                                          copies[i % ncopies][2]), args.steps, world)
     ms_loc, how_loc = _graph_or_eager(lambda i: copies[i % ncopies][0].run_local(copies[i % ncopies][1],
                                                                                 copies[i % ncopies][2]),
                                       args.steps, world)
-    # correctness after timing: every rank's Y is the whole product (TO_ALL)
-    P, dX, dY = copies[0]
+    ms_root, _ = _graph_or_eager(lambda i: copies[i % ncopies][3].run(copies[i % ncopies][1], copies[i % ncopies][2]),
+                                 args.steps, world)
+    # correctness after timing: every rank's Y is the whole product (TO_ALL),
+    # against the untiled row kernel (pinned to the reference by the tests;
+    # not the tiled kernel the ranks' shares run)
+    dl.enter("result check")
+    P, dX, dY, _ = copies[0]
     dY.fill_(float("nan"))
     P.run(dX, dY)
     torch.cuda.synchronize()
-    ref_plan = smfv.SpmmPlan(smfv.Variant.SEQUENTIAL, P.A, K)
+    ref_plan = smfv.SpmmPlan(smfv.Variant.SEQUENTIAL, P.A, K, tiles="off")
     Yseq = torch.empty_like(dY)
     ref_plan.run(dX, Yseq)
     mabs, _ = smfv.compare(Yseq, dY)
     ok = mabs == 0.0 if variant != "NONZERO" else mabs <= 1e-6
     # secondary: independent copies (every rank its own whole problem)
-    reps = [(smfv.SpmmPlan(smfv.Variant[variant], Pc.A, K, tiles=args.tiles), dXc, dYc) for Pc, dXc, dYc in copies]
+    reps = [(smfv.SpmmPlan(smfv.Variant[variant], Pc.A, K, tiles=args.tiles), dXc, dYc) for Pc, dXc, dYc, _ in copies]
     torch.cuda.synchronize()
     ms_rep, _ = _graph_or_eager(lambda i: reps[i % ncopies][0].run(reps[i % ncopies][1], reps[i % ncopies][2]),
                                 args.steps, world)
@@ -571,13 +643,14 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
             8 * _x_rows_touched(A, r0, r1) * K + 8 * (r1 - r0) * K
     else:
         loc_bytes = prob_bytes // world
-    t = torch.tensor([ms_step, ms_loc, ms_rep, float(loc_bytes) / max(ms_loc, 1e-9), 0.0 if ok else 1.0],
+    t = torch.tensor([ms_step, ms_loc, ms_rep, float(loc_bytes) / max(ms_loc, 1e-9), 0.0 if ok else 1.0, ms_root],
                      dtype=torch.float64)
     tmin = t.clone()
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(tmin, op=dist.ReduceOp.MIN)
-    ms_step, ms_loc, ms_rep, _, bad = t.tolist()
+    dl.cancel()
+    ms_step, ms_loc, ms_rep, _, bad, ms_root = t.tolist()
     flops = 2.0 * nnz * K
     st = P.stats()
     if rank == 0:
@@ -602,6 +675,11 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
                          "timing": f"rank-local kernel alone ({how_loc}), slowest rank"},
             "rank_local_ms": round(ms_loc, 6),
             "exchange_ms": round(ms_step - ms_loc, 6),
+            "exchange_ms_gather_to_root": round(ms_root - ms_loc, 6),
+            "exchange_note": "exchange_ms: all-gather of Y to every rank (the value's step); "
+                             "exchange_ms_gather_to_root: the reference's semantics, blocks gathered to rank 0 "
+                             "only (MPI_Gatherv, SC/...RowWise.cpp:85-87 / MPI_Reduce, ...NonZeroElement.cpp:88); "
+                             "each = (kernel + exchange) - kernel alone, max over ranks",
             "timing": how,
             "plan": {"create_s_total": round(t_plan, 3), "tiled": st["tiled"], "reuse": round(st["reuse"], 3)},
             "check": {"ok": not bad, "criterion": "Y on every rank vs the 1-GPU sequential plan, device compare "
@@ -616,7 +694,7 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     comm.close()
     if world > 1:
         dist.destroy_process_group()
-    if bad:
+    if bad and not args.no_check:
         sys.exit(3)
     return None
 
@@ -652,6 +730,9 @@ def main() -> None:
                     help="time the opt-in dense-block MFMA tile kernel (SMFV_PLAN_MFMA, config 3's MFMA K-panel)")
     ap.add_argument("--fma", action="store_true",
                     help="time the opt-in FMA plans (SMFV_PLAN_FMA) instead of the bit-exact ones")
+    ap.add_argument("--phase-timeout", type=float, default=240.0,
+                    help="multi-GPU paths: seconds a phase (RCCL set-up, plans, warm-up, timing, check) may take "
+                         "before a diagnostic JSON line and exit status 4 (0 = no watchdog)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

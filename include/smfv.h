@@ -73,6 +73,11 @@ typedef enum smfv_status {
 /* ---- library ------------------------------------------------------------ */
 SMFV_API const char *smfv_last_error(void);
 SMFV_API const char *smfv_version(void);
+/* Creates the HIP context on the current device and loads the library's
+ * code object (one empty kernel launch on `stream`, synchronised): the
+ * one-time device start-up a CPU caller never pays, done before a timed call
+ * so that call's time is the SpMM's. */
+SMFV_API int smfv_device_init(void *stream);
 
 /* ---- partitions (pure host functions, no device needed) ----------------- */
 /* RowWise: q = m/p, rows [r*q + min(r, m%p), +q + (r < m%p))  (RowWise.cpp:26-29) */
@@ -160,6 +165,12 @@ typedef struct smfv_plan_s *smfv_plan_t;
  * part as its own wavefront and runs part x on XCD x.  This flag keeps one
  * wavefront over the whole pattern cut into 8 consecutive shares (A/B). */
 #define SMFV_PLAN_ONE_WAVEFRONT 64
+/* Untiled, and the simplest row kernel for any K (one double per lane,
+ * k_rows): an independent computation of the same per-row sums, used by the
+ * C++ drop-in for the sequential function -- the result the parallel
+ * variants are checked against (SC/main.cpp:184) -- so that check does not
+ * compare a kernel with itself.  Ignored for SMFV_NONZERO. */
+#define SMFV_PLAN_SIMPLE_ROWS 128
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
 /* Plan of the row block [row_begin, row_end) of a CSR matrix (h_row_ptr /
@@ -169,6 +180,11 @@ SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int6
  * to d_Y (row i of the block at d_Y + i * ldy), as smfv_spmm_rowblock_f64. */
 SMFV_API int smfv_plan_create_rows(smfv_plan_t *plan, int variant, int row_begin, int row_end, int n,
                                    const int *h_row_ptr, const int *h_col_idx, int K, int flags);
+/* Host threads a plan analysis started on the CALLING thread may use (the
+ * tile analysis runs its 8 XCD parts in parallel): 0 = the default (up to 8);
+ * a library building plans in the background lowers it so the caller's own
+ * work keeps its cores. */
+SMFV_API void smfv_set_analysis_threads(int threads);
 SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, void *stream);
 /* Host-only diagnostic: run the clustered tile analysis and build the tiled
  * kernel's plan, verify the invariants the kernel relies on (every row in
@@ -338,6 +354,17 @@ SMFV_API int smfv_dist_rowpart_spmm_f64(smfv_comm_t comm, int mode, int root, in
 SMFV_API int smfv_dist_exchange_ops(int variant, int mode, int root, int m, int64_t nnz,
                                     const int *h_row_ptr, int K, int p, int rank, int *kinds, int *peers,
                                     int64_t *offsets, int64_t *counts, int *nops);
+/* Runs an exchange schedule (ops as smfv_dist_exchange_ops returns them, or
+ * any list of the same form) on `comm` over the device buffer d_buf:
+ * ncclAllGather alone, else one ncclGroupStart / ncclGroupEnd around the
+ * broadcasts / sends / receives.  A failing RCCL call closes the group
+ * before the error returns, so the communicator's next call starts clean.
+ * Collective; asynchronous on `stream`. */
+SMFV_API int smfv_comm_exchange_f64(smfv_comm_t comm, const int *kinds, const int *peers, const int64_t *offsets,
+                                    const int64_t *counts, int nops, double *d_buf, void *stream);
+/* Test hook: the nth exchange operation run from now on (any communicator,
+ * any plan) fails as an RCCL error would, inside its open group; 0 = off. */
+SMFV_API void smfv_test_fail_exchange(int nth);
 
 /* ---- distributed plans: the rank-local part analysed once --------------
  * A distributed plan holds this rank's share of a variant (RowWise row
@@ -358,6 +385,18 @@ SMFV_API int smfv_dist_plan_create(smfv_dist_plan_t *plan, smfv_comm_t comm, int
 SMFV_API int smfv_dist_plan_create_rowpart(smfv_dist_plan_t *plan, smfv_comm_t comm, int mode, int root, int m,
                                            int n, const int *h_row_ptr_local, const int *h_col_idx_local, int K,
                                            int flags);
+/* The plan of rank `rank` of `p` with no communicator: the rank-local share
+ * exactly as a rank of smfv_dist_plan_create computes it (same partition,
+ * same single-device plan), execute_local only -- exchange and execute
+ * return SMFV_ERR_COMM when the schedule has operations.  Lets one device
+ * run every rank of a p-rank decomposition (tests, replays). */
+SMFV_API int smfv_dist_plan_create_rank(smfv_dist_plan_t *plan, int p, int rank, int variant, int mode, int root,
+                                        int m, int n, int64_t nnz, const int *h_row_ptr, const int *h_col_idx, int K,
+                                        int flags);
+/* The plan's exchange buffer (device; COLUMNWISE rank-major panels, NONZERO
+ * compact row blocks, at smfv_dist_plan's offset / count) and its size in
+ * doubles; NULL / 0 for ROWWISE, whose exchange runs in Y. */
+SMFV_API int smfv_dist_plan_exchange_buffer(smfv_dist_plan_t plan, double **d_buf, int64_t *doubles);
 SMFV_API int smfv_dist_plan_bind_values(smfv_dist_plan_t plan, const double *d_values, void *stream);
 SMFV_API int smfv_dist_plan_execute(smfv_dist_plan_t plan, const int *d_row_ptr, const int *d_col_idx,
                                     const double *d_values, const double *d_X, double *d_Y, void *stream);

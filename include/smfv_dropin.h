@@ -20,20 +20,54 @@
 
 #include "MatrixDefinitions.h"
 
+//   smfvInitDevice         the one-time device start-up (HIP context, code
+//                          object load) a CPU caller never pays, done before
+//                          the first timed call
+//   smfvLastCallTiming     the stage times of the last call (SMFV_TIMING=1)
+
+// Creates the HIP context on this rank's GPU and loads the library's code
+// object.  Returns its wall time (seconds).  Optional: the first call does
+// it otherwise, inside its own time.
+double smfvInitDevice();
+
 // Collective over MPI_COMM_WORLD.  Rank 0's A and fatVector (n x k) are
 // uploaded once and broadcast device-to-device; the other ranks' A and
 // fatVector are overwritten with rank 0's.  Until smfvReleaseInputs(), calls
 // of the four functions with these SAME objects (same addresses, same
-// sizes) use the resident device copies instead of uploading A and X again:
-// the caller must not modify them in between.  Returns the wall time of the
-// distribution (seconds, rank-local).
+// sizes) use the resident device copies instead of uploading A and X again.
+// Each such call compares the objects with host snapshots taken here (exact,
+// a parallel memcmp) and uploads again any array the caller has changed in
+// between, so a call never computes with stale inputs.  Returns the wall
+// time of the distribution (seconds, rank-local).
 double smfvDistributeInputs(SparseMatrix &A, FatVector &fatVector, int k);
 void smfvReleaseInputs();
 
+// Stage times (seconds) of the last call of the four functions on this rank,
+// recorded when the environment has SMFV_TIMING=1 (then rank 0 also prints
+// them, averaged over the ranks for the MPI variants, as the reference's
+// debug build did: "<Variant> Average Computation Time: t" / "... Average
+// Communication Time: t", SC/...RowWise.cpp:96-108, plus the host
+// preparation, H2D, D2H and FatVector rebuild stages).  The stages follow
+// each other, so they account for `total` up to the host's launch gaps.
+struct SmfvCallTiming {
+    double prep;           // checks, serialize / resident-input verification, plan lookup (host)
+    double h2d;            // uploads of A and X (device, hipEvents; ~0 when resident and unchanged)
+    double compute;        // values bind + the rank-local kernels (device, hipEvents)
+    double communication;  // the RCCL exchange (device, hipEvents; 0 on one rank)
+    double d2h;            // D2H of Y (device, hipEvents; 0 off the root)
+    double rebuild;        // the FatVector rebuild (host)
+    double total;          // the call, wall clock
+};
+SmfvCallTiming smfvLastCallTiming();
+
 // Rank 0: keep the device result of the last call (e.g. the serial one) as
 // the reference.  smfvCompareWithReference: areMatricesEqual(reference,
-// last result, tolerance) evaluated on the device (max |a - b|, NaN counts as
-// a difference); *max_abs_diff receives the maximum (may be NULL).  Both
+// last result, tolerance) evaluated on the device (max |a - b|); a NaN
+// difference counts as a difference here -- stricter than the reference's
+// areMatricesEqual, whose `fabs(a - b) > tolerance` test is false for NaN
+// (SC/utils.cpp:55) and so passes it; the host areMatricesEqual of
+// libsmfv_mpi.so keeps the reference's behaviour.  *max_abs_diff receives
+// the maximum (may be NULL).  Both
 // apply to rank 0's last result; on other ranks they return false / do
 // nothing.
 void smfvKeepResultAsReference();

@@ -41,6 +41,7 @@ _PI64 = POINTER(c_int64)
 _SIGS = {
     "smfv_last_error": (c_char_p, []),
     "smfv_version": (c_char_p, []),
+    "smfv_device_init": (c_int, [c_void_p]),
     "smfv_partition_rows": (None, [c_int, c_int, c_int, _PI, _PI]),
     "smfv_partition_cols": (None, [c_int, c_int, c_int, _PI, _PI]),
     "smfv_partition_nnz": (None, [c_int64, c_int, c_int, _PI64, _PI64]),
@@ -55,6 +56,7 @@ _SIGS = {
                                       c_int]),
     "smfv_plan_analyse": (c_int, [c_int, c_int, _PI, _PI, _PD]),
     "smfv_plan_analyse_rows": (c_int, [c_int, c_int, c_int, _PI, _PI, c_int, _PD]),
+    "smfv_set_analysis_threads": (None, [c_int]),
     "smfv_plan_bind_values": (c_int, [c_void_p, c_void_p, c_void_p]),
     "smfv_plan_execute": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                   c_void_p, c_int64, c_void_p]),
@@ -97,6 +99,11 @@ _SIGS = {
                                       _PI, _PI, c_int, c_int]),
     "smfv_dist_plan_create_rowpart": (c_int, [POINTER(c_void_p), c_void_p, c_int, c_int, c_int, c_int, _PI, _PI,
                                               c_int, c_int]),
+    "smfv_dist_plan_create_rank": (c_int, [POINTER(c_void_p), c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                           c_int64, _PI, _PI, c_int, c_int]),
+    "smfv_dist_plan_exchange_buffer": (c_int, [c_void_p, POINTER(_PD), _PI64]),
+    "smfv_comm_exchange_f64": (c_int, [c_void_p, _PI, _PI, _PI64, _PI64, c_int, c_void_p, c_void_p]),
+    "smfv_test_fail_exchange": (None, [c_int]),
     "smfv_dist_plan_bind_values": (c_int, [c_void_p, c_void_p, c_void_p]),
     "smfv_dist_plan_execute": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "smfv_dist_plan_execute_local": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -10,12 +10,12 @@
 // plus the extensions of include/smfv_dropin.h (device-resident inputs,
 // device-side result check).
 //
-// Every call goes through a PLAN cached by matrix pattern (variant, sizes,
-// K, world size and a 64-bit hash of rowPtr and colIndices): the first call
-// on a pattern analyses it (the tiled kernel's row tiles, or the rank's
-// share of a distributed variant); later calls only bind the values and
-// launch.  A call therefore runs the same kernels the bench times
-// (k_rows_ws where the pattern re-uses X rows).
+// Every call goes through a PLAN cached by matrix pattern (see "plan cache"
+// below): the first call on a pattern runs at once on an untiled plan while
+// the tiled plan is analysed on a background thread; later calls take the
+// tiled plan (k_rows_ws where the pattern re-uses X rows, the kernel the
+// bench times) and only bind the values and launch.  SMFV_TIMING=1 prints
+// each call's stage times in the reference's debug-line format.
 //
 // Device placement: rank r of MPI_COMM_WORLD uses GPU (local rank % devices).
 // The RCCL communicator is created on first collective use (rank 0 makes the
@@ -24,11 +24,19 @@
 #include <hip/hip_runtime.h>
 #include <mpi.h>
 
+#include <sys/resource.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -145,6 +153,7 @@ struct Cached {
 
 struct Buffers {
     Cached rp, ci, va, X, Y, ref, hX{nullptr, 0, true}, hY{nullptr, 0, true};
+    Cached hrp{nullptr, 0, true}, hci{nullptr, 0, true}, hva{nullptr, 0, true};  // pinned A staging
     // the result of the last call on this rank (device) and the kept reference
     const double *lastY = nullptr;
     int last_m = -1, last_K = -1, ref_m = -1, ref_K = -1;
@@ -202,23 +211,174 @@ uint64_t hash_bytes(const void *data, size_t bytes)
     return h;
 }
 
+// element-wise equality of host ranges, in parallel chunks
+bool par_equal(const void *a, const void *b, size_t bytes)
+{
+    if (bytes < (1u << 20)) return std::memcmp(a, b, bytes) == 0;
+    std::atomic<bool> same{true};
+    const char *x = static_cast<const char *>(a), *y = static_cast<const char *>(b);
+    par_rows((int64_t)(bytes >> 16) + 1, [&](int64_t lo, int64_t hi) {
+        const size_t s = (size_t)lo << 16, e = std::min(bytes, (size_t)hi << 16);
+        if (s < e && same.load(std::memory_order_relaxed) && std::memcmp(x + s, y + s, e - s)) same = false;
+    });
+    return same;
+}
+
+// ---- per-stage timing (SMFV_TIMING=1) ------------------------------------
+// The reference's debug build timed each variant's local computation and
+// its communication on every rank and printed their averages over the ranks
+// (SC/...RowWise.cpp:21-23, 52-60, 89-109; ...ColumnWise.cpp:20-22, 50-58,
+// 86-106; ...NonZeroElement.cpp:19-21, 69-77, 90-109), scraped by
+// SC/scripts/get_csv_debug.sh.  Here a call is cut into five stages that
+// follow each other: host preparation (checks, serialize / input
+// verification, plan lookup), H2D, compute (values bind + the rank-local
+// kernels), communication (the RCCL exchange), D2H, FatVector rebuild.
+// Device stages are timed by hipEvents on the call's stream, host stages by
+// the wall clock; together they account for the call's wall time.
+bool timing_on()
+{
+    static const bool on = [] {
+        const char *e = std::getenv("SMFV_TIMING");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+
+struct StageTimer {
+    bool on = timing_on();
+    // [0] before H2D, [1] before compute, [2] before exchange, [3] before D2H, [4] after D2H
+    hipEvent_t ev[5] = {};
+    double t_begin = 0, t_prep = 0, t_synced = 0;
+    SmfvCallTiming out{};
+    StageTimer()
+    {
+        if (!on) return;
+        t_begin = MPI_Wtime();
+        for (auto &e : ev) hip_check(hipEventCreate(&e), "hipEventCreate");
+    }
+    ~StageTimer()
+    {
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+    void mark(int i, hipStream_t st)
+    {
+        if (!on) return;
+        if (i == 0) t_prep = MPI_Wtime();
+        hip_check(hipEventRecord(ev[i], st), "hipEventRecord");
+    }
+    // after the stream has been synchronised (Y on the host), before the rebuild
+    void device_done()
+    {
+        if (!on) return;
+        t_synced = MPI_Wtime();
+        float ms[4] = {0, 0, 0, 0};
+        for (int i = 0; i < 4; ++i) hip_check(hipEventElapsedTime(&ms[i], ev[i], ev[i + 1]), "hipEventElapsedTime");
+        out.prep = t_prep - t_begin;
+        out.h2d = ms[0] * 1e-3;
+        out.compute = ms[1] * 1e-3;
+        out.communication = ms[2] * 1e-3;
+        out.d2h = ms[3] * 1e-3;
+    }
+    void finish()
+    {
+        if (!on) return;
+        const double end = MPI_Wtime();
+        out.rebuild = end - t_synced;
+        out.total = end - t_begin;
+    }
+};
+
+SmfvCallTiming g_last_timing{};
+
+// rank 0 prints the stage times of a call in the reference's debug-line
+// format (averages over the ranks, as its MPI_Reduce(SUM) / worldSize)
+void report_timing(const char *name, const SmfvCallTiming &t, bool collective)
+{
+    SmfvCallTiming avg = t;
+    const Context &c = g_ctx;
+    if (collective && c.mpi && c.size > 1) {
+        double loc[7] = {t.prep, t.h2d, t.compute, t.communication, t.d2h, t.rebuild, t.total}, sum[7] = {0};
+        MPI_Reduce(loc, sum, 7, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);
+        avg.prep = sum[0] / c.size;
+        avg.h2d = sum[1] / c.size;
+        avg.compute = sum[2] / c.size;
+        avg.communication = sum[3] / c.size;
+        avg.d2h = sum[4] / c.size;
+        avg.rebuild = sum[5] / c.size;
+        avg.total = sum[6] / c.size;
+    }
+    g_last_timing = t;
+    if (c.rank != 0) return;
+    std::printf("%s Average Computation Time: %g\n", name, avg.compute);
+    std::printf("%s Average Communication Time: %g\n", name, avg.communication);
+    std::printf("%s Host Preparation Time: %g\n", name, avg.prep);
+    std::printf("%s Host-to-Device Time: %g\n", name, avg.h2d);
+    std::printf("%s Device-to-Host Time: %g\n", name, avg.d2h);
+    std::printf("%s FatVector Rebuild Time: %g\n", name, avg.rebuild);
+    std::fflush(stdout);
+}
+
 // inputs distributed by smfvDistributeInputs: device copies kept resident
-// (own buffers: a call with other inputs does not overwrite them)
+// (own buffers: a call with other inputs does not overwrite them), with
+// host snapshots of what was distributed.  A call with the same objects
+// compares them against the snapshots (exact, parallel memcmp) and uploads
+// again whatever the caller changed, so resident inputs are never stale.
 struct Resident {
     bool on = false;
     const SparseMatrix *A = nullptr;
     const FatVector *fat = nullptr;
-    const double *va_host = nullptr;
-    const int *ci_host = nullptr, *rp_host = nullptr;
-    size_t nnz = 0, rows = 0;
     int m = 0, n = 0, K = 0;
+    int64_t nnz = 0;
     uint64_t hrp = 0, hci = 0;
-    Cached rp, ci, va, X;
+    uint64_t values_version = 0;  // bumped when the device values change
+    std::vector<int> rp, ci;
+    std::vector<double> va, X;  // snapshots (X row-major flat)
+    Cached drp, dci, dva, dX;
     bool matches(const SparseMatrix &Am, const FatVector &f, int K_) const
     {
-        return on && &Am == A && &f == fat && K_ == K && Am.values.data() == va_host &&
-               Am.colIndices.data() == ci_host && Am.rowPtr.data() == rp_host && Am.values.size() == nnz &&
-               Am.numRows == m && Am.numCols == n && f.size() == rows;
+        return on && &Am == A && &f == fat && K_ == K && Am.numRows == m && Am.numCols == n &&
+               (int64_t)Am.values.size() == nnz && (int64_t)Am.colIndices.size() == nnz &&
+               Am.rowPtr.size() == rp.size() && (int)f.size() == n;
+    }
+    // compare with the caller's current host objects (host preparation),
+    // then re-upload what changed (the H2D stage, opened by T.mark(0))
+    void refresh(const SparseMatrix &Am, const FatVector &f, hipStream_t st, StageTimer &T)
+    {
+        const bool rp_new = !par_equal(Am.rowPtr.data(), rp.data(), rp.size() * sizeof(int));
+        const bool ci_new = !par_equal(Am.colIndices.data(), ci.data(), ci.size() * sizeof(int));
+        const bool va_new = !par_equal(Am.values.data(), va.data(), va.size() * sizeof(double));
+        std::atomic<bool> xsame{true};
+        par_rows(n, [&](int64_t a, int64_t b) {
+            for (int64_t i = a; i < b && xsame.load(std::memory_order_relaxed); ++i)
+                if ((int)f[i].size() != K || std::memcmp(f[i].data(), X.data() + (size_t)i * K, (size_t)K * 8))
+                    xsame = false;
+        });
+        if (rp_new) rp = Am.rowPtr;
+        if (ci_new) ci = Am.colIndices;
+        if (rp_new || ci_new) {
+            hrp = hash_bytes(rp.data(), rp.size() * sizeof(int));
+            hci = hash_bytes(ci.data(), ci.size() * sizeof(int));
+        }
+        if (va_new) {
+            va = Am.values;
+            ++values_version;
+        }
+        if (!xsame) {
+            for (const auto &r : f)
+                if ((int)r.size() != K) fail("fatVector rows must have vecCols entries");
+            par_rows(n, [&](int64_t a, int64_t b) {
+                for (int64_t i = a; i < b; ++i) std::copy(f[i].begin(), f[i].end(), X.data() + (size_t)i * K);
+            });
+        }
+        T.mark(0, st);
+        auto up = [&](void *d, const void *h, size_t bytes) {
+            if (bytes) hip_check(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+        };
+        if (rp_new) up(drp.p, rp.data(), rp.size() * sizeof(int));
+        if (ci_new) up(dci.p, ci.data(), ci.size() * sizeof(int));
+        if (va_new) up(dva.p, va.data(), va.size() * sizeof(double));
+        if (!xsame) up(dX.p, X.data(), X.size() * sizeof(double));
     }
 };
 
@@ -228,6 +388,8 @@ Resident &resident()
     return *r;
 }
 
+uint64_t g_upload_version = 0;  // values uploaded by a non-resident call (always new)
+
 // A and X on the device for one call
 struct Problem {
     int m, n, K;
@@ -235,7 +397,9 @@ struct Problem {
     int *rp, *ci;
     double *va, *X, *Y;
     uint64_t hrp = 0, hci = 0;  // pattern hashes (plan cache key)
-    Problem(const SparseMatrix &A, const FatVector &fat, int K_, hipStream_t st)
+    uint64_t values_id = 0;     // identifies the device values' content (skip an unchanged re-bind)
+    const int *h_rp, *h_ci;     // the host pattern (verified against a cached plan's copy)
+    Problem(const SparseMatrix &A, const FatVector &fat, int K_, hipStream_t st, StageTimer &T)
         : m(A.numRows), n(A.numCols), K(K_), nnz((int64_t)A.values.size())
     {
         if ((int)A.rowPtr.size() != m + 1 || (int64_t)A.colIndices.size() != nnz ||
@@ -245,14 +409,19 @@ struct Problem {
             fail("fatVector has " + std::to_string(fat.size()) + " rows, matrix has " + std::to_string(n) + " columns");
         Buffers &B = bufs();
         Y = static_cast<double *>(B.Y.get((size_t)m * K * sizeof(double)));
+        (void)B.hY.get((size_t)m * K * sizeof(double));  // pinned Y staging (allocated here, in preparation)
         Resident &R = resident();
-        if (R.matches(A, fat, K)) {  // device-resident inputs: nothing to upload
-            rp = static_cast<int *>(R.rp.p);
-            ci = static_cast<int *>(R.ci.p);
-            va = static_cast<double *>(R.va.p);
-            X = static_cast<double *>(R.X.p);
+        if (R.matches(A, fat, K)) {  // device-resident inputs: upload only what the caller changed
+            R.refresh(A, fat, st, T);
+            rp = static_cast<int *>(R.drp.p);
+            ci = static_cast<int *>(R.dci.p);
+            va = static_cast<double *>(R.dva.p);
+            X = static_cast<double *>(R.dX.p);
             hrp = R.hrp;
             hci = R.hci;
+            h_rp = R.rp.data();
+            h_ci = R.ci.data();
+            values_id = (R.values_version << 1) | 1;
             return;
         }
         for (const auto &r : fat)
@@ -261,28 +430,48 @@ struct Problem {
         ci = static_cast<int *>(B.ci.get(A.colIndices.size() * sizeof(int)));
         va = static_cast<double *>(B.va.get(A.values.size() * sizeof(double)));
         X = static_cast<double *>(B.X.get((size_t)n * K * sizeof(double)));
-        // serialize (SC/utils.cpp:216-228) straight into pinned staging
+        // serialize (SC/utils.cpp:216-228) straight into pinned staging, and
+        // A's arrays too: the DMA then runs at pinned-copy speed (a pageable
+        // source is copied through a driver bounce buffer at a fraction of it)
         double *hx = static_cast<double *>(B.hX.get((size_t)n * K * sizeof(double)));
         par_rows(n, [&](int64_t a, int64_t b) {
             for (int64_t i = a; i < b; ++i) std::copy(fat[i].begin(), fat[i].end(), hx + (size_t)i * K);
         });
+        auto stage = [&](Cached &c, const void *src, size_t bytes) -> const void * {
+            void *h = c.get(bytes);
+            par_rows((int64_t)(bytes >> 16) + 1, [&](int64_t lo, int64_t hi) {
+                const size_t s0 = (size_t)lo << 16, e0 = std::min(bytes, (size_t)hi << 16);
+                if (s0 < e0) std::memcpy(static_cast<char *>(h) + s0, static_cast<const char *>(src) + s0, e0 - s0);
+            });
+            return h;
+        };
+        const void *hrp_ = stage(B.hrp, A.rowPtr.data(), A.rowPtr.size() * sizeof(int));
+        const void *hci_ = stage(B.hci, A.colIndices.data(), A.colIndices.size() * sizeof(int));
+        const void *hva_ = stage(B.hva, A.values.data(), A.values.size() * sizeof(double));
+        hrp = hash_bytes(A.rowPtr.data(), A.rowPtr.size() * sizeof(int));
+        hci = hash_bytes(A.colIndices.data(), A.colIndices.size() * sizeof(int));
+        h_rp = A.rowPtr.data();
+        h_ci = A.colIndices.data();
+        values_id = (++g_upload_version) << 1;
+        T.mark(0, st);
         auto up = [&](void *d, const void *h, size_t bytes) {
             if (bytes) hip_check(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
         };
-        up(rp, A.rowPtr.data(), A.rowPtr.size() * sizeof(int));
-        up(ci, A.colIndices.data(), A.colIndices.size() * sizeof(int));
-        up(va, A.values.data(), A.values.size() * sizeof(double));
+        up(rp, hrp_, A.rowPtr.size() * sizeof(int));
+        up(ci, hci_, A.colIndices.size() * sizeof(int));
+        up(va, hva_, A.values.size() * sizeof(double));
         up(X, hx, (size_t)n * K * sizeof(double));
-        hrp = hash_bytes(A.rowPtr.data(), A.rowPtr.size() * sizeof(int));
-        hci = hash_bytes(A.colIndices.data(), A.colIndices.size() * sizeof(int));
     }
-    FatVector download(hipStream_t st)
+    FatVector download(hipStream_t st, StageTimer &T)
     {
         double *hy = static_cast<double *>(bufs().hY.get((size_t)m * K * sizeof(double)));
+        T.mark(3, st);
         if ((size_t)m * K)
             hip_check(hipMemcpyAsync(hy, Y, (size_t)m * K * sizeof(double), hipMemcpyDeviceToHost, st),
                       "hipMemcpyAsync");
+        T.mark(4, st);
         hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+        T.device_done();
         // deserialize (SC/utils.cpp:238-253): the m row vectors built in parallel
         FatVector out((size_t)m);
         par_rows(m, [&](int64_t a, int64_t b) {
@@ -299,7 +488,24 @@ struct Problem {
     }
 };
 
-// plan cache (least recently used out; a plan holds device memory)
+// ---- plan cache --------------------------------------------------------------
+// A call's plan comes from a cache keyed by (variant, sizes, K, world size,
+// 64-bit hashes of rowPtr and colIndices); a key match is confirmed by
+// comparing the call's pattern with the copy the entry keeps (a hash
+// collision never runs another pattern's plan).
+//
+// First call on a pattern: it runs at once on an UNTILED plan (no pattern
+// analysis: the row / merge kernels, tens of microseconds on cop20k_A) while
+// the tiled plan -- the row-tile analysis, a one-time host cost of tens to
+// hundreds of milliseconds -- is built on a background thread at low
+// priority from the entry's own copy of the pattern.  Later calls take the
+// tiled plan as soon as it is ready (k_rows_ws where the pattern re-uses X
+// rows), the untiled one until then.  So no call waits for a plan analysis,
+// and a caller that calls once (the reference's main.cpp) gets the first-call
+// time of an SpMM, not of a setup.  SEQUENTIAL always runs the simplest row
+// kernel (SMFV_PLAN_SIMPLE_ROWS, one double per lane): it is the result the
+// parallel variants are checked against (SC/main.cpp:184), so the check
+// never compares a kernel with itself.
 struct PlanKey {
     int variant, m, n, K, world;
     int64_t nnz;
@@ -310,78 +516,222 @@ struct PlanKey {
                hrp == o.hrp && hci == o.hci;
     }
 };
-struct PlanEntry {
-    PlanKey key;
+
+struct Plans {  // one plan of a variant: single-device or distributed
     smfv_plan_t local = nullptr;
     smfv_dist_plan_t dist = nullptr;
+    void destroy()
+    {
+        if (local) smfv_plan_destroy(local);
+        if (dist) smfv_dist_plan_destroy(dist);
+        local = nullptr;
+        dist = nullptr;
+    }
+    bool tiled() const
+    {
+        double st[SMFV_PLAN_STATS] = {0};
+        if (local) smfv_plan_stats(local, st);
+        if (dist) smfv_dist_plan_stats(dist, st);
+        return st[0] != 0.0;
+    }
+};
+
+struct PlanEntry {
+    PlanKey key;
+    std::vector<int> rp, ci;        // the pattern this entry's plans were built for
+    Plans untiled;                  // created with the entry (SMFV_PLAN_NO_TILES)
+    Plans tiled;                    // the background build's result, once taken
+    std::future<Plans> building;    // the background build (valid until taken)
+    bool build_pending = false;     // to be started when the current call has returned its result
+    int world = 1, device = 0;
+    bool tiled_ready = false;
     uint64_t used = 0;
+    uint64_t bound_values = 0;      // Problem::values_id last bound into `tiled`
+    ~PlanEntry()
+    {
+        if (building.valid()) {  // never leave a thread writing into a dead entry
+            Plans p = building.get();
+            p.destroy();
+        }
+        untiled.destroy();
+        tiled.destroy();
+    }
 };
 constexpr size_t kMaxPlans = 8;
 
-std::vector<PlanEntry> &plans()
+std::vector<std::unique_ptr<PlanEntry>> &plans()
 {
-    static auto *v = new std::vector<PlanEntry>;
+    static auto *v = new std::vector<std::unique_ptr<PlanEntry>>;
     return *v;
 }
 
-PlanEntry &plan_for(int variant, const SparseMatrix &A, const Problem &P, int world)
+// at exit: let running background builds finish and free their plans
+// while the HIP runtime is still up (registered after it initialised, so
+// this runs before its teardown)
+void join_background_builds()
+{
+    for (auto &e : plans())
+        if (e->building.valid()) {
+            Plans p = e->building.get();
+            p.destroy();
+        }
+}
+
+Plans create_plans(int variant, int m, int n, int64_t nnz, const int *rp, const int *ci, int K, int world,
+                   int flags, int device)
+{
+    Plans p;
+    if (hipSetDevice(device) != hipSuccess) return p;  // (a background thread starts on device 0)
+    int rc;
+    if (world == 1)
+        rc = smfv_plan_create(&p.local, variant, m, n, nnz, rp, ci, K, flags);
+    else
+        rc = smfv_dist_plan_create(&p.dist, comm_world(), variant, SMFV_TO_ROOT, 0, m, n, nnz, rp, ci, K, flags);
+    if (rc != SMFV_OK) p.destroy();
+    return p;
+}
+
+// The cache entry of this call's (variant, pattern), created on a miss.
+PlanEntry &plan_for(int variant, const Problem &P, int world)
 {
     static uint64_t tick = 0;
-    // on one rank SEQUENTIAL / ROWWISE / COLUMNWISE are the same computation
-    // (bit-identical per-row sums): they share one plan
-    if (world == 1 && variant != SMFV_NONZERO) variant = SMFV_ROWWISE;
-    const PlanKey key{variant, P.m, P.n, P.K, world, P.nnz, P.hrp, P.hci};
+    // on one rank ROWWISE / COLUMNWISE are the same computation (bit-identical
+    // per-row sums): they share one plan
+    if (world == 1 && variant == SMFV_COLUMNWISE) variant = SMFV_ROWWISE;
+    // test hook: SMFV_TEST_PLAN_KEY_BITS=b keeps only b bits of the pattern
+    // hashes (0: every pattern of equal sizes collides), so the tests can show
+    // that a key match is confirmed against the stored pattern
+    static const uint64_t key_mask = [] {
+        const char *e = std::getenv("SMFV_TEST_PLAN_KEY_BITS");
+        const int b = e ? std::atoi(e) : 64;
+        return b >= 64 ? ~0ull : b <= 0 ? 0ull : ((1ull << b) - 1);
+    }();
+    const PlanKey key{variant, P.m, P.n, P.K, world, P.nnz, P.hrp & key_mask, P.hci & key_mask};
     auto &v = plans();
-    for (auto &e : v)
-        if (e.key == key) {
-            e.used = ++tick;
-            return e;
+    PlanEntry *e = nullptr;
+    for (auto &x : v)
+        if (x->key == key && par_equal(x->rp.data(), P.h_rp, x->rp.size() * sizeof(int)) &&
+            par_equal(x->ci.data(), P.h_ci, x->ci.size() * sizeof(int))) {
+            e = x.get();
+            break;
         }
-    if (v.size() >= kMaxPlans) {
-        auto lru = std::min_element(v.begin(), v.end(), [](const PlanEntry &a, const PlanEntry &b) { return a.used < b.used; });
-        if (lru->local) smfv_plan_destroy(lru->local);
-        if (lru->dist) smfv_dist_plan_destroy(lru->dist);
-        v.erase(lru);
+    if (!e) {
+        if (v.size() >= kMaxPlans) {
+            auto lru = std::min_element(v.begin(), v.end(),
+                                        [](const auto &a, const auto &b) { return a->used < b->used; });
+            v.erase(lru);  // (waits for its background build, if any)
+        }
+        auto ne = std::make_unique<PlanEntry>();
+        ne->key = key;
+        ne->rp.assign(P.h_rp, P.h_rp + P.m + 1);
+        ne->ci.assign(P.h_ci, P.h_ci + P.nnz);
+        if (world > 1) (void)comm_world();  // the communicator exists before any thread needs it
+        int dev = 0;
+        hip_check(hipGetDevice(&dev), "hipGetDevice");
+        ne->untiled = create_plans(variant, P.m, P.n, P.nnz, ne->rp.data(), ne->ci.data(), P.K, world,
+                                   SMFV_PLAN_NO_TILES | (variant == SMFV_SEQUENTIAL ? SMFV_PLAN_SIMPLE_ROWS : 0), dev);
+        if (!ne->untiled.local && !ne->untiled.dist) check(SMFV_ERR_INVALID, "smfv plan create (untiled)");
+        const bool may_tile = variant != SMFV_SEQUENTIAL && P.K % 32 == 0 && P.m > 0 && P.nnz > 0;
+        if (may_tile) {
+            ne->build_pending = true;  // started by start_pending_builds() once this call is done
+            ne->world = world;
+            ne->device = dev;
+        } else {
+            ne->tiled_ready = true;  // nothing to build: the untiled plan is the plan
+        }
+        v.push_back(std::move(ne));
+        e = v.back().get();
     }
-    PlanEntry e;
-    e.key = key;
-    e.used = ++tick;
-    if (world == 1)
-        check(smfv_plan_create(&e.local, variant, P.m, P.n, P.nnz, A.rowPtr.data(), A.colIndices.data(), P.K, 0),
-              "smfv_plan_create");
-    else
-        check(smfv_dist_plan_create(&e.dist, comm_world(), variant, SMFV_TO_ROOT, 0, P.m, P.n, P.nnz, A.rowPtr.data(),
-                                    A.colIndices.data(), P.K, 0),
-              "smfv_dist_plan_create");
-    v.push_back(e);
-    return v.back();
+    e->used = ++tick;
+    if (!e->tiled_ready && e->building.valid() &&
+        e->building.wait_for(std::chrono::seconds(0)) == std::future_status::ready) {
+        e->tiled = e->building.get();
+        e->tiled_ready = true;
+        if (!e->tiled.tiled()) e->tiled.destroy();  // the analysis decided not to tile: keep the untiled plan
+    }
+    return *e;
 }
 
-FatVector local_run(int variant, const SparseMatrix &A, const FatVector &fat, int K)
+// Starts the background analyses of entries created by this call, after its
+// result is on the host: the analysis (<= 4 threads, nice 10) then overlaps
+// the caller's own work between calls, not the call's FatVector rebuild.
+void start_pending_builds()
+{
+    for (auto &x : plans()) {
+        PlanEntry *raw = x.get();
+        if (!raw->build_pending) continue;
+        raw->build_pending = false;
+        static const bool registered = std::atexit(join_background_builds) == 0;
+        (void)registered;
+        raw->building = std::async(std::launch::async, [raw]() {
+            setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), 10);  // behind the caller's own work
+            smfv_set_analysis_threads(4);
+            return create_plans(raw->key.variant, raw->key.m, raw->key.n, raw->key.nnz, raw->rp.data(),
+                                raw->ci.data(), raw->key.K, raw->world, 0, raw->device);
+        });
+    }
+}
+
+// The entry's plan to run (tiled once built), bound to the call's values.
+Plans &bound_plan(PlanEntry *e, const Problem &P, hipStream_t st)
+{
+    const bool use_tiled = e->tiled.local || e->tiled.dist;
+    Plans &pl = use_tiled ? e->tiled : e->untiled;
+    if (use_tiled && e->bound_values != P.values_id) {  // the tiled plan's values snapshot
+        if (pl.local) check(smfv_plan_bind_values(pl.local, P.va, st), "smfv_plan_bind_values");
+        else check(smfv_dist_plan_bind_values(pl.dist, P.va, st), "smfv_dist_plan_bind_values");
+        e->bound_values = P.values_id;
+    } else if (!use_tiled) {
+        if (pl.local) check(smfv_plan_bind_values(pl.local, P.va, st), "smfv_plan_bind_values");
+        else check(smfv_dist_plan_bind_values(pl.dist, P.va, st), "smfv_dist_plan_bind_values");
+    }
+    return pl;
+}
+
+FatVector local_run(int variant, const SparseMatrix &A, const FatVector &fat, int K, const char *name)
 {
     Context &c = ctx();
-    Problem P(A, fat, K, c.stream);
-    PlanEntry &e = plan_for(variant, A, P, 1);
-    check(smfv_plan_bind_values(e.local, P.va, c.stream), "smfv_plan_bind_values");
-    check(smfv_plan_execute(e.local, P.rp, P.ci, P.va, P.X, K, P.Y, K, c.stream), "smfv_plan_execute");
+    StageTimer T;
+    Problem P(A, fat, K, c.stream, T);
+    PlanEntry &e = plan_for(variant, P, 1);
+    T.mark(1, c.stream);
+    Plans &pl = bound_plan(&e, P, c.stream);
+    check(smfv_plan_execute(pl.local, P.rp, P.ci, P.va, P.X, K, P.Y, K, c.stream), "smfv_plan_execute");
+    T.mark(2, c.stream);
     P.note_result();
-    return P.download(c.stream);
+    FatVector out = P.download(c.stream, T);
+    T.finish();
+    start_pending_builds();
+    if (T.on) report_timing(name, T.out, false);
+    return out;
 }
 
-FatVector collective_run(int variant, const SparseMatrix &A, const FatVector &fat, int K)
+FatVector collective_run(int variant, const SparseMatrix &A, const FatVector &fat, int K, const char *name)
 {
     Context &c = ctx();
-    if (c.size == 1) return local_run(variant, A, fat, K);
-    Problem P(A, fat, K, c.stream);
-    PlanEntry &e = plan_for(variant, A, P, c.size);
-    check(smfv_dist_plan_bind_values(e.dist, P.va, c.stream), "smfv_dist_plan_bind_values");
-    check(smfv_dist_plan_execute(e.dist, P.rp, P.ci, P.va, P.X, P.Y, c.stream), "smfv_dist_plan_execute");
+    if (c.size == 1) return local_run(variant, A, fat, K, name);
+    StageTimer T;
+    Problem P(A, fat, K, c.stream, T);
+    PlanEntry &e = plan_for(variant, P, c.size);
+    T.mark(1, c.stream);
+    Plans &pl = bound_plan(&e, P, c.stream);
+    check(smfv_dist_plan_execute_local(pl.dist, P.rp, P.ci, P.va, P.X, P.Y, c.stream), "smfv_dist_plan_execute_local");
+    T.mark(2, c.stream);
+    check(smfv_dist_plan_exchange(pl.dist, P.Y, c.stream), "smfv_dist_plan_exchange");
+    FatVector out;
     if (c.rank != 0) {
+        T.mark(3, c.stream);
+        T.mark(4, c.stream);
         hip_check(hipStreamSynchronize(c.stream), "hipStreamSynchronize");
-        return FatVector{};
+        T.device_done();
+    } else {
+        P.note_result();
+        out = P.download(c.stream, T);
     }
-    P.note_result();
-    return P.download(c.stream);
+    T.finish();
+    start_pending_builds();
+    if (T.on) report_timing(name, T.out, true);
+    return out;
 }
 
 }  // namespace
@@ -389,28 +739,38 @@ FatVector collective_run(int variant, const SparseMatrix &A, const FatVector &fa
 DROPIN_API FatVector sparseMatrixFatVectorMultiply(const SparseMatrix &sparseMatrix,
                                                    const FatVector &fatVector, int vecCols)
 {
-    return local_run(SMFV_SEQUENTIAL, sparseMatrix, fatVector, vecCols);
+    return local_run(SMFV_SEQUENTIAL, sparseMatrix, fatVector, vecCols, "Serial Algo");
 }
 
 DROPIN_API FatVector sparseMatrixFatVectorMultiplyRowWise(const SparseMatrix &sparseMatrix,
                                                           const FatVector &fatVector, int vecCols)
 {
-    return collective_run(SMFV_ROWWISE, sparseMatrix, fatVector, vecCols);
+    return collective_run(SMFV_ROWWISE, sparseMatrix, fatVector, vecCols, "Row-wise");
 }
 
 DROPIN_API FatVector sparseMatrixFatVectorMultiplyColumnWise(const SparseMatrix &sparseMatrix,
                                                              const FatVector &fatVector, int vecCols)
 {
-    return collective_run(SMFV_COLUMNWISE, sparseMatrix, fatVector, vecCols);
+    return collective_run(SMFV_COLUMNWISE, sparseMatrix, fatVector, vecCols, "Column-wise");
 }
 
 DROPIN_API FatVector sparseMatrixFatVectorMultiplyNonZeroElement(const SparseMatrix &sparseMatrix,
                                                                  const FatVector &fatVector, int vecCols)
 {
-    return collective_run(SMFV_NONZERO, sparseMatrix, fatVector, vecCols);
+    return collective_run(SMFV_NONZERO, sparseMatrix, fatVector, vecCols, "Non-zero elements");
 }
 
 // ---- extensions (include/smfv_dropin.h) -------------------------------------
+
+DROPIN_API double smfvInitDevice()
+{
+    const double t0 = MPI_Wtime();
+    Context &c = ctx();
+    check(smfv_device_init(c.stream), "smfv_device_init");
+    return MPI_Wtime() - t0;
+}
+
+DROPIN_API SmfvCallTiming smfvLastCallTiming() { return g_last_timing; }
 
 DROPIN_API double smfvDistributeInputs(SparseMatrix &A, FatVector &fat, int k)
 {
@@ -425,10 +785,10 @@ DROPIN_API double smfvDistributeInputs(SparseMatrix &A, FatVector &fat, int k)
     if (m < 0 || n < 0 || nnz < 0 || K < 0) fail("smfvDistributeInputs: bad sizes");
     Resident &R = resident();
     R.on = false;
-    int *rp = static_cast<int *>(R.rp.get(((size_t)m + 1) * sizeof(int)));
-    int *ci = static_cast<int *>(R.ci.get((size_t)nnz * sizeof(int)));
-    double *va = static_cast<double *>(R.va.get((size_t)nnz * sizeof(double)));
-    double *X = static_cast<double *>(R.X.get((size_t)n * K * sizeof(double)));
+    int *rp = static_cast<int *>(R.drp.get(((size_t)m + 1) * sizeof(int)));
+    int *ci = static_cast<int *>(R.dci.get((size_t)nnz * sizeof(int)));
+    double *va = static_cast<double *>(R.dva.get((size_t)nnz * sizeof(double)));
+    double *X = static_cast<double *>(R.dX.get((size_t)n * K * sizeof(double)));
     Buffers &B = bufs();
     double *hx = static_cast<double *>(B.hX.get((size_t)n * K * sizeof(double)));
     hipStream_t st = c.stream;
@@ -475,23 +835,33 @@ DROPIN_API double smfvDistributeInputs(SparseMatrix &A, FatVector &fat, int k)
         });
     }
     hip_check(hipStreamSynchronize(st), "hipStreamSynchronize");
+    // host snapshots of what is resident (each call compares against them)
     R.A = &A;
     R.fat = &fat;
-    R.va_host = A.values.data();
-    R.ci_host = A.colIndices.data();
-    R.rp_host = A.rowPtr.data();
-    R.nnz = (size_t)nnz;
-    R.rows = fat.size();
     R.m = m;
     R.n = n;
     R.K = K;
-    R.hrp = hash_bytes(A.rowPtr.data(), A.rowPtr.size() * sizeof(int));
-    R.hci = hash_bytes(A.colIndices.data(), A.colIndices.size() * sizeof(int));
+    R.nnz = nnz;
+    R.rp = A.rowPtr;
+    R.ci = A.colIndices;
+    R.va = A.values;
+    R.X.assign(hx, hx + (size_t)n * K);
+    R.hrp = hash_bytes(R.rp.data(), R.rp.size() * sizeof(int));
+    R.hci = hash_bytes(R.ci.data(), R.ci.size() * sizeof(int));
+    ++R.values_version;
     R.on = true;
     return MPI_Wtime() - t0;
 }
 
-DROPIN_API void smfvReleaseInputs() { resident().on = false; }
+DROPIN_API void smfvReleaseInputs()
+{
+    Resident &R = resident();
+    R.on = false;
+    R.rp = {};
+    R.ci = {};
+    R.va = {};
+    R.X = {};
+}
 
 DROPIN_API void smfvKeepResultAsReference()
 {

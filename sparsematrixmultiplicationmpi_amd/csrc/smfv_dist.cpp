@@ -46,7 +46,26 @@ namespace {
         }                                                                                   \
     } while (0)
 
+// the same inside ncclGroupStart / ncclGroupEnd: a failing call closes the
+// group before returning, so the communicator's next collective starts clean
+#define SMFV_NCCL_IN_GROUP(call)                                                            \
+    do {                                                                                    \
+        ncclResult_t r_ = (call);                                                           \
+        if (r_ != ncclSuccess) {                                                            \
+            (void)ncclGroupEnd();                                                           \
+            ::smfv::set_error("%s failed: %s (%s:%d)", #call, ncclGetErrorString(r_),       \
+                              __FILE__, __LINE__);                                          \
+            return SMFV_ERR_COMM;                                                           \
+        }                                                                                   \
+    } while (0)
+
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// test hook (smfv_test_fail_exchange): the n-th exchange operation run by
+// run_exchange fails as an RCCL error would, inside its open group -- the
+// error path is exercised without a broken interconnect
+long g_fail_exchange = 0;
+bool injected_failure() { return g_fail_exchange > 0 && --g_fail_exchange == 0; }
 
 }  // namespace
 
@@ -238,11 +257,20 @@ static std::vector<ExOp> exchange_schedule(const Plan &P, int p, int rank, bool 
 }
 
 // Runs a schedule with RCCL on `st` (one group; the all-gather alone).
+// comm == NULL (a rank plan, smfv_dist_plan_create_rank) runs no exchange.
 static int run_exchange(smfv_comm_t comm, const std::vector<ExOp> &ops, double *xbuf, hipStream_t st)
 {
     if (ops.empty()) return SMFV_OK;
+    if (!comm) {
+        set_error("exchange needs a communicator (this plan was created for one rank alone)");
+        return SMFV_ERR_COMM;
+    }
     if (ops.size() == 1 && ops[0].kind == SMFV_EX_ALLGATHER) {
         const ExOp &o = ops[0];
+        if (injected_failure()) {
+            set_error("ncclAllGather failed: injected test failure (SMFV_TEST_FAIL_EXCHANGE)");
+            return SMFV_ERR_COMM;
+        }
         // block r lands at offset - rank * count + r * count
         SMFV_NCCL(ncclAllGather(xbuf + o.offset, xbuf + o.offset - (int64_t)comm->rank * o.count, (size_t)o.count,
                                 ncclDouble, comm->nccl, st));
@@ -252,10 +280,15 @@ static int run_exchange(smfv_comm_t comm, const std::vector<ExOp> &ops, double *
     for (const ExOp &o : ops) {
         double *blk = xbuf + o.offset;
         const size_t cnt = (size_t)o.count;
+        if (injected_failure()) {
+            (void)ncclGroupEnd();
+            set_error("exchange op %d failed: injected test failure (smfv_test_fail_exchange)", o.kind);
+            return SMFV_ERR_COMM;
+        }
         switch (o.kind) {
-        case SMFV_EX_BCAST: SMFV_NCCL(ncclBroadcast(blk, blk, cnt, ncclDouble, o.peer, comm->nccl, st)); break;
-        case SMFV_EX_RECV: SMFV_NCCL(ncclRecv(blk, cnt, ncclDouble, o.peer, comm->nccl, st)); break;
-        case SMFV_EX_SEND: SMFV_NCCL(ncclSend(blk, cnt, ncclDouble, o.peer, comm->nccl, st)); break;
+        case SMFV_EX_BCAST: SMFV_NCCL_IN_GROUP(ncclBroadcast(blk, blk, cnt, ncclDouble, o.peer, comm->nccl, st)); break;
+        case SMFV_EX_RECV: SMFV_NCCL_IN_GROUP(ncclRecv(blk, cnt, ncclDouble, o.peer, comm->nccl, st)); break;
+        case SMFV_EX_SEND: SMFV_NCCL_IN_GROUP(ncclSend(blk, cnt, ncclDouble, o.peer, comm->nccl, st)); break;
         default: (void)ncclGroupEnd(); set_error("bad exchange op %d", o.kind); return SMFV_ERR_INVALID;
         }
     }
@@ -290,6 +323,25 @@ SMFV_API int smfv_dist_exchange_ops(int variant, int mode, int root, int m, int6
     *nops = (int)ops.size();
     return SMFV_OK;
 }
+
+SMFV_API int smfv_comm_exchange_f64(smfv_comm_t comm, const int *kinds, const int *peers, const int64_t *offsets,
+                                    const int64_t *counts, int nops, double *d_buf, void *stream)
+{
+    SMFV_REQUIRE(comm && nops >= 0 && (nops == 0 || (kinds && peers && offsets && counts && d_buf)), "bad argument");
+    std::vector<ExOp> ops((size_t)nops);
+    for (int i = 0; i < nops; ++i) {
+        SMFV_REQUIRE(kinds[i] >= SMFV_EX_ALLGATHER && kinds[i] <= SMFV_EX_RECV, "bad op kind %d", kinds[i]);
+        SMFV_REQUIRE(offsets[i] >= 0 && counts[i] >= 0, "bad op range");
+        SMFV_REQUIRE(kinds[i] == SMFV_EX_ALLGATHER || (peers[i] >= 0 && peers[i] < comm->nranks), "bad peer %d",
+                     peers[i]);
+        SMFV_REQUIRE(kinds[i] != SMFV_EX_ALLGATHER || (nops == 1 && offsets[i] >= (int64_t)comm->rank * counts[i]),
+                     "an all-gather op runs alone and its blocks start at offset - rank * count >= 0");
+        ops[(size_t)i] = {kinds[i], peers[i], offsets[i], counts[i]};
+    }
+    return run_exchange(comm, ops, d_buf, smfv::as_stream(stream));
+}
+
+SMFV_API void smfv_test_fail_exchange(int nth) { g_fail_exchange = nth > 0 ? nth : 0; }
 
 SMFV_API int smfv_dist_spmm_f64(smfv_comm_t comm, int variant, int mode, int root, int m, int n,
                                 int64_t nnz, const int *h_row_ptr, const int *d_row_ptr,
@@ -382,7 +434,8 @@ SMFV_API int smfv_dist_rowpart_spmm_f64(smfv_comm_t comm, int mode, int root, in
 // distributed plans
 // ---------------------------------------------------------------------------
 struct smfv_dist_plan_s {
-    smfv_comm_t comm = nullptr;
+    smfv_comm_t comm = nullptr;   // NULL: a rank plan (smfv_dist_plan_create_rank), no exchange
+    int p = 1, rank = 0;          // this plan's rank of p
     int variant = 0, mode = 0, root = 0, m = 0, n = 0, K = 0;
     bool rowpart = false;
     Plan P;
@@ -398,8 +451,7 @@ struct smfv_dist_plan_s {
 
 static int dist_plan_finish(smfv_dist_plan_s *d, smfv_dist_plan_t *out)
 {
-    const int p = d->comm->nranks, rank = d->comm->rank;
-    d->ops = exchange_schedule(d->P, p, rank, d->variant != SMFV_NONZERO, d->mode == SMFV_TO_ALL, d->root);
+    d->ops = exchange_schedule(d->P, d->p, d->rank, d->variant != SMFV_NONZERO, d->mode == SMFV_TO_ALL, d->root);
     if (d->variant == SMFV_COLUMNWISE || d->variant == SMFV_NONZERO) {
         const size_t b = std::max<size_t>((size_t)d->P.total, 1) * sizeof(double);
         hipError_t e = hipMalloc(reinterpret_cast<void **>(&d->xbuf), b);
@@ -413,17 +465,21 @@ static int dist_plan_finish(smfv_dist_plan_s *d, smfv_dist_plan_t *out)
     return SMFV_OK;
 }
 
-SMFV_API int smfv_dist_plan_create(smfv_dist_plan_t *out, smfv_comm_t comm, int variant, int mode, int root, int m,
-                                   int n, int64_t nnz, const int *h_row_ptr, const int *h_col_idx, int K, int flags)
+// rank `rank` of `p` (comm may be NULL: a rank plan without exchange)
+static int dist_plan_create(smfv_dist_plan_t *out, smfv_comm_t comm, int p, int rank, int variant, int mode,
+                            int root, int m, int n, int64_t nnz, const int *h_row_ptr, const int *h_col_idx, int K,
+                            int flags)
 {
-    SMFV_REQUIRE(out && comm && h_row_ptr, "null plan / communicator / row_ptr");
+    SMFV_REQUIRE(out && h_row_ptr, "null plan / row_ptr");
+    SMFV_REQUIRE(p > 0 && rank >= 0 && rank < p, "bad rank %d of %d", rank, p);
     SMFV_REQUIRE(mode == SMFV_TO_ROOT || mode == SMFV_TO_ALL, "bad mode %d", mode);
-    SMFV_REQUIRE(root >= 0 && root < comm->nranks, "bad root %d", root);
+    SMFV_REQUIRE(root >= 0 && root < p, "bad root %d", root);
     SMFV_REQUIRE(m >= 0 && n >= 0 && nnz >= 0 && nnz <= 0x7fffffff && K >= 0 && h_row_ptr[m] == nnz, "bad sizes");
     SMFV_REQUIRE(variant >= SMFV_SEQUENTIAL && variant <= SMFV_NONZERO, "unknown variant %d", variant);
-    const int p = comm->nranks, rank = comm->rank;
     auto *d = new smfv_dist_plan_s;
     d->comm = comm;
+    d->p = p;
+    d->rank = rank;
     d->variant = variant == SMFV_SEQUENTIAL ? SMFV_ROWWISE : variant;
     d->mode = mode;
     d->root = root;
@@ -444,7 +500,7 @@ SMFV_API int smfv_dist_plan_create(smfv_dist_plan_t *out, smfv_comm_t comm, int 
             int64_t s, e;
             smfv_partition_nnz(nnz, p, rank, &s, &e);
             rc = smfv::plan_create(&d->local, SMFV_NONZERO, f, std::max(0, l - f + 1), n, s, e, nullptr, nullptr, K,
-                                   flags);
+                                   flags, f);
         }
         }
     }
@@ -453,6 +509,21 @@ SMFV_API int smfv_dist_plan_create(smfv_dist_plan_t *out, smfv_comm_t comm, int 
         return rc;
     }
     return dist_plan_finish(d, out);
+}
+
+SMFV_API int smfv_dist_plan_create(smfv_dist_plan_t *out, smfv_comm_t comm, int variant, int mode, int root, int m,
+                                   int n, int64_t nnz, const int *h_row_ptr, const int *h_col_idx, int K, int flags)
+{
+    SMFV_REQUIRE(comm, "null communicator");
+    return dist_plan_create(out, comm, comm->nranks, comm->rank, variant, mode, root, m, n, nnz, h_row_ptr, h_col_idx,
+                            K, flags);
+}
+
+SMFV_API int smfv_dist_plan_create_rank(smfv_dist_plan_t *out, int p, int rank, int variant, int mode, int root,
+                                        int m, int n, int64_t nnz, const int *h_row_ptr, const int *h_col_idx, int K,
+                                        int flags)
+{
+    return dist_plan_create(out, nullptr, p, rank, variant, mode, root, m, n, nnz, h_row_ptr, h_col_idx, K, flags);
 }
 
 SMFV_API int smfv_dist_plan_create_rowpart(smfv_dist_plan_t *out, smfv_comm_t comm, int mode, int root, int m, int n,
@@ -464,6 +535,8 @@ SMFV_API int smfv_dist_plan_create_rowpart(smfv_dist_plan_t *out, smfv_comm_t co
     SMFV_REQUIRE(m >= 0 && n >= 0 && K >= 0, "bad sizes");
     auto *d = new smfv_dist_plan_s;
     d->comm = comm;
+    d->p = comm->nranks;
+    d->rank = comm->rank;
     d->variant = SMFV_ROWWISE;
     d->rowpart = true;
     d->mode = mode;
@@ -472,15 +545,26 @@ SMFV_API int smfv_dist_plan_create_rowpart(smfv_dist_plan_t *out, smfv_comm_t co
     d->n = n;
     d->K = K;
     int rc = make_plan(SMFV_ROWWISE, m, 0, nullptr, K, comm->nranks, d->P);
-    const int mloc = d->P.last[comm->rank] - d->P.first[comm->rank] + 1;
+    const int first = d->P.first[comm->rank];
+    const int mloc = d->P.last[comm->rank] - first + 1;
+    // the local rows are global rows first.., so the pattern's column c is
+    // local row c - first: the tile analysis' neighbours (col_base = first)
     if (!rc)
-        rc = smfv_plan_create(&d->local, SMFV_ROWWISE, mloc, n, h_row_ptr_local[mloc], h_row_ptr_local,
-                              h_col_idx_local, K, flags);
+        rc = smfv::plan_create(&d->local, SMFV_ROWWISE, 0, mloc, n, 0, h_row_ptr_local[mloc], h_row_ptr_local,
+                               h_col_idx_local, K, flags, first);
     if (rc) {
         delete d;
         return rc;
     }
     return dist_plan_finish(d, out);
+}
+
+SMFV_API int smfv_dist_plan_exchange_buffer(smfv_dist_plan_t d, double **d_buf, int64_t *doubles)
+{
+    SMFV_REQUIRE(d && d_buf && doubles, "null argument");
+    *d_buf = d->xbuf;
+    *doubles = d->xbuf ? d->P.total : 0;
+    return SMFV_OK;
 }
 
 SMFV_API int smfv_dist_plan_bind_values(smfv_dist_plan_t d, const double *d_values, void *stream)
@@ -494,7 +578,7 @@ SMFV_API int smfv_dist_plan_execute_local(smfv_dist_plan_t d, const int *d_row_p
 {
     SMFV_REQUIRE(d, "null plan");
     SMFV_REQUIRE(d_Y || d->m == 0 || d->K == 0, "null Y");
-    const int rank = d->comm->rank, K = d->K;
+    const int rank = d->rank, K = d->K;
     const int f = d->P.first[rank], l = d->P.last[rank];
     switch (d->variant) {
     case SMFV_ROWWISE:  // in place: this rank's rows of Y
@@ -520,8 +604,8 @@ SMFV_API int smfv_dist_plan_exchange(smfv_dist_plan_t d, double *d_Y, void *stre
     double *buf = d->variant == SMFV_ROWWISE ? d_Y : d->xbuf;
     int rc = run_exchange(d->comm, d->ops, buf, st);
     if (rc) return rc;
-    const int p = d->comm->nranks;
-    if (!(d->mode == SMFV_TO_ALL || d->comm->rank == d->root)) return SMFV_OK;
+    const int p = d->p;
+    if (!(d->mode == SMFV_TO_ALL || d->rank == d->root)) return SMFV_OK;
     if (d->variant == SMFV_COLUMNWISE) return smfv_panels_to_rowmajor_f64(d->m, d->K, p, d->xbuf, d_Y, d->K, stream);
     if (d->variant == SMFV_NONZERO)
         return smfv_combine_row_blocks_f64(d->m, d->K, p, d->P.first.data(), d->P.last.data(), d->xbuf, d_Y, d->K,

@@ -47,7 +47,11 @@ size_t merge_workspace_bytes(int nrows, int64_t nnz, int K);
 // smfv_plan_create / smfv_plan_create_rows with an explicit non-zero range
 // (NONZERO rank-local plans: rows [row_begin, row_begin + m) restricted to
 // the non-zeros [nnz_base, nnz_end)); h_rp / h_ci: the whole matrix or NULL.
+// col_base: the global row of the block's first row, for a square pattern's
+// neighbour lookup in the tile analysis (column c = block row c - col_base);
+// -1 = row_begin (the block is a slice of the whole matrix), a local CSR of
+// a row partition passes its first global row.
 int plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n, int64_t nnz_base, int64_t nnz_end,
-                const int *h_rp, const int *h_ci, int K, int flags);
+                const int *h_rp, const int *h_ci, int K, int flags, int col_base = -1);
 
 }  // namespace smfv

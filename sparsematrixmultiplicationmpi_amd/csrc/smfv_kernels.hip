@@ -851,6 +851,9 @@ __global__ __launch_bounds__(256) void k_copy16(int64_t n16, const ws::d2 *__res
         if (base + 256 * k < n16) __builtin_nontemporal_store(a[k], dst + base + 256 * k);
 }
 
+// smfv_device_init: loads the code object, computes nothing
+__global__ void k_noop() {}
+
 // plan value binding: tile-ordered copy of A's values (pads -> pad)
 __global__ __launch_bounds__(256) void k_gather_vals(int64_t count, const int *__restrict__ tsrc,
                                                      const double *__restrict__ va,
@@ -1252,6 +1255,9 @@ static int launch_rows_mh(int row_begin, int nrows, const int *rp, const int *ci
     return SMFV_ERR_INVALID;
 }
 
+static int launch_rows_simple(int row_begin, int nrows, const int *rp, const int *ci, const double *va,
+                              const double *X, int64_t ldx, int K, double *Y, int64_t ldy, hipStream_t st);
+
 static int launch_rows(int row_begin, int nrows, const int *rp, const int *ci, const double *va,
                        const double *X, int64_t ldx, int64_t xrows, int K, double *Y, int64_t ldy,
                        hipStream_t st)
@@ -1272,7 +1278,15 @@ static int launch_rows(int row_begin, int nrows, const int *rp, const int *ci, c
     }
     const int vec = pick_vec(X, ldx, Y, ldy, K);
     if (vec == 2) return launch_rows_mh(row_begin, nrows, rp, ci, va, X, ldx, xrows, K, Y, ldy, st);
-    // odd K or unaligned X / Y: one double per lane, shuffle-broadcast kernel
+    return launch_rows_simple(row_begin, nrows, rp, ci, va, X, ldx, K, Y, ldy, st);
+}
+
+// odd K, unaligned X / Y, or a plan with SMFV_PLAN_SIMPLE_ROWS: one double
+// per lane, the team's (col, val) pairs broadcast by shuffle (k_rows)
+static int launch_rows_simple(int row_begin, int nrows, const int *rp, const int *ci, const double *va,
+                              const double *X, int64_t ldx, int K, double *Y, int64_t ldy, hipStream_t st)
+{
+    if (nrows <= 0 || K <= 0) return SMFV_OK;
     const int team = pick_team(K, 1);
     const int rpb = 256 / team;
     const int64_t nblk = ((int64_t)nrows + rpb - 1) / rpb;
@@ -1368,6 +1382,15 @@ SMFV_API const char *smfv_last_error(void) { return g_last_error.c_str(); }
 
 SMFV_API const char *smfv_version(void) { return "smfv 0.1.0 gfx950"; }
 
+SMFV_API int smfv_device_init(void *stream)
+{
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, st);
+    SMFV_LAUNCHED();
+    SMFV_HIP(hipStreamSynchronize(st));
+    return SMFV_OK;
+}
+
 SMFV_API void smfv_partition_rows(int m, int p, int r, int *start, int *end)
 {
     const int q = m / p, extra = m % p;
@@ -1462,30 +1485,37 @@ constexpr int SMFV_TILE_SAMPLE_MIN_ROWS = 16384;  // below this the full analysi
 constexpr int SMFV_WS_BLOCKS_PER_XCD = 32;        // k_rows_ws blocks per XCD on MI355X (256 CUs)
 constexpr int SMFV_WS_CHUNKED = 0;                // k_rows_ws tile order per block: 0 strided, 1 consecutive runs
 
-// The tile caps a plan with these flags uses for the row block (row_begin,
-// m rows; rp block-local, ci from the block's first non-zero).
-static TileCaps plan_caps(int flags, int row_begin, int m, int n, const int *rp, const int *ci, double *footprint)
+// The tile caps a plan with these flags uses for the row block whose first
+// row is global row col_base (its neighbour lookup), before the XCD parts.
+static TileCaps plan_caps(int flags, int col_base)
 {
     TileCaps caps;
     caps.frontier = !(flags & SMFV_PLAN_NATURAL_SEEDS);
     caps.split_ends = (flags & SMFV_PLAN_SPLIT_ENDS) ? SMFV_WS_BLOCKS_PER_XCD : 0;
-    caps.col_base = row_begin;  // a row block's neighbours are its columns shifted by row_begin
-    *footprint = -1.0;
-    if (caps.frontier && m > 0 && !(flags & (SMFV_PLAN_ONE_WAVEFRONT | SMFV_PLAN_SPLIT_ENDS | SMFV_PLAN_MFMA))) {
-        // one part per XCD: the row ranges or the breadth-first shares,
-        // whichever reads fewer X rows over the 8 L2s
-        std::vector<int> br, bs;
-        range_parts(m, rp, 8, caps.part_rows, caps.part_start);
-        bfs_parts(m, rp, ci, row_begin, 8, br, bs);
-        const double fr = parts_footprint(m, n, rp, ci, caps.part_rows, caps.part_start);
-        const double fb = parts_footprint(m, n, rp, ci, br, bs);
-        *footprint = std::min(fr, fb);
-        if (fb < fr) {
-            caps.part_rows.swap(br);
-            caps.part_start.swap(bs);
-        }
-    }
+    caps.col_base = col_base;  // a row block's neighbours are its columns shifted by its first global row
     return caps;
+}
+
+// The XCD parts of a tiled plan (m rows; rp block-local, ci from the block's
+// first non-zero): one part per XCD -- the row ranges or the breadth-first
+// shares, whichever reads fewer X rows over the 8 L2s.  Run only once the
+// plan is known to tile (the BFS and the footprints are O(nnz) passes with
+// n-sized stamp arrays).
+static void plan_parts(TileCaps &caps, int flags, int m, int n, const int *rp, const int *ci, double *footprint)
+{
+    *footprint = -1.0;
+    if (!caps.frontier || m <= 0 || (flags & (SMFV_PLAN_ONE_WAVEFRONT | SMFV_PLAN_SPLIT_ENDS | SMFV_PLAN_MFMA)))
+        return;
+    std::vector<int> br, bs;
+    range_parts(m, rp, 8, caps.part_rows, caps.part_start);
+    bfs_parts(m, rp, ci, caps.col_base, 8, br, bs);
+    const double fr = parts_footprint(m, n, rp, ci, caps.part_rows, caps.part_start);
+    const double fb = parts_footprint(m, n, rp, ci, br, bs);
+    *footprint = std::min(fr, fb);
+    if (fb < fr) {
+        caps.part_rows.swap(br);
+        caps.part_start.swap(bs);
+    }
 }
 
 struct smfv_plan_s {
@@ -1493,6 +1523,7 @@ struct smfv_plan_s {
     int row_begin = 0;                     // first CSR row of the plan's row block
     int64_t nnz_base = 0, nnz_end = 0;     // the block's CSR range [row_ptr[row_begin], row_ptr[row_end])
     bool fma = false;  // SMFV_PLAN_FMA: fused multiply-add in the tiled kernel (not bit-identical)
+    bool simple = false;  // SMFV_PLAN_SIMPLE_ROWS: untiled, one double per lane (k_rows<TEAM, 1>)
     int64_t nnz = 0;                       // non-zeros of the block
     bool tiled = false;
     int ntiles = 0, ndirect = 0;
@@ -1541,11 +1572,14 @@ template <class T> int upload(T **dst, const std::vector<T> &src, size_t &acc)
 // indexes the whole matrix's values.  NONZERO plans cover the non-zeros
 // [nnz_base, nnz_end) of the block's rows (a rank's nnz range).
 int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n, int64_t nnz_base, int64_t nnz_end,
-                const int *h_rp, const int *h_ci, int K, int flags)
+                const int *h_rp, const int *h_ci, int K, int flags, int col_base)
 {
+    if (col_base < 0) col_base = row_begin;
     const auto t_start = std::chrono::steady_clock::now();
     auto *p = new smfv_plan_s;
     p->fma = (flags & SMFV_PLAN_FMA) != 0;
+    p->simple = (flags & SMFV_PLAN_SIMPLE_ROWS) != 0 && variant != SMFV_NONZERO;
+    if (p->simple) flags |= SMFV_PLAN_NO_TILES;
     p->variant = variant;
     p->row_begin = row_begin;
     p->m = m;
@@ -1584,10 +1618,10 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
         for (int i = 0; i <= m; ++i) rpl[i] = (int)(h_rp[row_begin + i] - nnz_base);
         const int *cil = h_ci + nnz_base;
         bool go = true;
-        const TileCaps caps = plan_caps(flags, row_begin, m, n, rpl.data(), cil, &p->footprint);
+        TileCaps caps = plan_caps(flags, col_base);
         if (!(flags & SMFV_PLAN_FORCE_TILES) && m > SMFV_TILE_SAMPLE_MIN_ROWS) {
-            // estimate re-use on the first tiles before the full analysis
-            // (which costs O(nnz * candidates))
+            // estimate re-use on the first tiles (frontier-grown in the full
+            // pattern, one part) before any O(nnz) pass of the full analysis
             TileCaps sc = caps;
             sc.max_tiles = SMFV_TILE_SAMPLE_TILES;
             TileAnalysis T;
@@ -1595,6 +1629,7 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
             p->est_reuse = T.union_rows ? (double)T.tiled_nnz / (double)T.union_rows : 0.0;
             go = p->est_reuse >= SMFV_TILE_MIN_REUSE;
         }
+        if (go) plan_parts(caps, flags, m, n, rpl.data(), cil, &p->footprint);
         if (go && (flags & SMFV_PLAN_MFMA)) {
             MfmaPlan F;
             std::string err;
@@ -1729,7 +1764,8 @@ SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int
     const int *h_row_ptr = rpl.data();
     const int *h_col_idx = h_col_idx_all ? h_col_idx_all + h_row_ptr_all[row_begin] : nullptr;
     double footprint = -1.0;
-    const TileCaps caps = plan_caps(flags, row_begin, m, n, h_row_ptr, h_col_idx, &footprint);
+    TileCaps caps = plan_caps(flags, row_begin);
+    plan_parts(caps, flags, m, n, h_row_ptr, h_col_idx, &footprint);
     TileAnalysis T;
     analyse_tiles(m, n, h_row_ptr, h_col_idx, T, caps);
     // invariants of the clustered analysis the plan is built from
@@ -1799,6 +1835,8 @@ SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int
     out[8] = total ? (double)sum / (double)total : 0.0;
     return SMFV_OK;
 }
+
+SMFV_API void smfv_set_analysis_threads(int threads) { smfv::analysis_threads = threads > 0 ? threads : 0; }
 
 SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, void *stream)
 {
@@ -1873,6 +1911,8 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         if (plan->variant == SMFV_NONZERO)
             return launch_merge(plan->row_begin, m, plan->nnz_base, plan->nnz_end, d_row_ptr, d_col_idx, d_values,
                                 d_X, ldx, K, d_Y, ldy, plan->ws, plan->ws_bytes, st);
+        if (plan->simple)
+            return launch_rows_simple(plan->row_begin, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, K, d_Y, ldy, st);
         return launch_rows(plan->row_begin, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, plan->n, K, d_Y, ldy, st);
     }
     if (d_values != plan->bound_values) {

@@ -14,29 +14,258 @@
 #include "smfv_plan.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 
 namespace smfv {
+
+thread_local int analysis_threads = 0;
+
+namespace {
+
+// Rows that hold each column (the pattern's transpose, O(nnz) to build):
+// `all` lists a row once per entry (multiplicity kept: the in-tile
+// neighbour count of a candidate counts entries), `dist` once per column.
+struct ColumnRows {
+    std::vector<int64_t> ptr, dptr;
+    std::vector<int> all, dist;
+    void build(int m, int n, const int *rp, const int *ci)
+    {
+        const int nc = std::max(n, 1);
+        ptr.assign((size_t)nc + 1, 0);
+        dptr.assign((size_t)nc + 1, 0);
+        for (int r = 0; r < m; ++r)
+            for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                ++ptr[(size_t)ci[j] + 1];
+                if (j == rp[r] || ci[j] != ci[j - 1]) ++dptr[(size_t)ci[j] + 1];  // rows are column-sorted
+            }
+        for (int c = 0; c < nc; ++c) ptr[c + 1] += ptr[c], dptr[c + 1] += dptr[c];
+        all.resize((size_t)ptr[(size_t)nc]);
+        dist.resize((size_t)dptr[(size_t)nc]);
+        std::vector<int64_t> fa(ptr.begin(), ptr.end() - 1), fd(dptr.begin(), dptr.end() - 1);
+        for (int r = 0; r < m; ++r)
+            for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                all[(size_t)fa[(size_t)ci[j]]++] = r;
+                if (j == rp[r] || ci[j] != ci[j - 1]) dist[(size_t)fd[(size_t)ci[j]]++] = r;
+            }
+    }
+};
+
+// Per-thread state of the greedy (column- and row-indexed stamps).
+struct TileScratch {
+    std::vector<int> ustamp, upos, cstamp, rstamp, fresh, inner;
+    std::vector<int64_t> probe;
+    int64_t probe_id = 0;
+    TileScratch(int m, int n)
+        : ustamp((size_t)std::max(n, 1), -1), upos((size_t)std::max(n, 1), 0), cstamp((size_t)std::max(m, 1), -1),
+          rstamp((size_t)std::max(m, 1), -1), fresh((size_t)std::max(m, 1), 0), inner((size_t)std::max(m, 1), 0),
+          probe((size_t)std::max(n, 1), -1)
+    {
+    }
+};
+
+// The tiles of one part (positions [lo, hi) of the row order P), appended to
+// A with tile ids starting at `tile`; stops after max_tiles tiles in all
+// (> 0).  Candidate scores are kept up to date as the tile grows (the union
+// gains a column: its rows' fresh counts drop; the tile gains a row: the
+// rows naming it gain an in-tile neighbour), so a step costs a scan of the
+// candidates' scores, not of their rows.  Returns false when max_tiles ended it.
+bool analyse_part(int part, int lo, int hi, const int *P, int m, const int *rp, const int *ci, const ColumnRows &T,
+                  const std::vector<int> &pid, const std::vector<int> &ppos, std::vector<char> &assigned,
+                  TileScratch &S, TileAnalysis &A, int &tile, const TileCaps &caps)
+{
+    std::vector<int> cand, rows, front;
+    size_t fhead = 0;
+    int next_free = 0;
+    for (int scan = lo; scan < hi;) {
+        int seed = -1;
+        if (caps.frontier)
+            while (fhead < front.size() && seed < 0) {
+                const int r = front[fhead++];
+                if (!assigned[r]) seed = r;
+            }
+        if (seed < 0) {
+            while (scan < hi && assigned[P[scan]]) ++scan;
+            if (scan >= hi) break;
+            seed = P[scan];
+        }
+        if (caps.max_tiles > 0 && tile >= caps.max_tiles) return false;
+        next_free = ppos[(size_t)seed] + 1;  // position after the seed in its part
+        int ucount = 0;
+        int64_t tnnz = 0, tpad = 0;  // real and row-padded non-zeros
+        rows.clear();
+        cand.clear();
+        const size_t ubase = A.ucols.size();
+        // a row's score terms against the current tile, from scratch
+        auto score_terms = [&](int r) {
+            ++S.probe_id;
+            int fresh = 0, inner = 0;
+            for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                const int c = ci[j];
+                const int cr = c - caps.col_base;
+                if (cr >= 0 && cr < m && S.rstamp[cr] == tile) ++inner;
+                if (S.ustamp[c] != tile && S.probe[c] != S.probe_id) {
+                    S.probe[c] = S.probe_id;
+                    ++fresh;
+                }
+            }
+            S.fresh[r] = fresh;
+            S.inner[r] = inner;
+        };
+        auto add_row = [&](int r) {
+            assigned[r] = 1;
+            S.rstamp[r] = tile;
+            rows.push_back(r);
+            tnnz += rp[r + 1] - rp[r];
+            tpad += (rp[r + 1] - rp[r] + caps.pad - 1) & ~(caps.pad - 1);
+            // union grows: the candidates holding a new column need one fresh row less
+            for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                const int c = ci[j];
+                if (S.ustamp[c] == tile) continue;
+                S.ustamp[c] = tile;
+                S.upos[c] = ucount++;
+                A.ucols.push_back(c);
+                for (int64_t q = T.dptr[(size_t)c]; q < T.dptr[(size_t)c + 1]; ++q) {
+                    const int x = T.dist[(size_t)q];
+                    if (S.cstamp[x] == tile && !assigned[x]) --S.fresh[x];
+                }
+            }
+            // r joins the tile: the candidates naming it gain an in-tile neighbour
+            const int64_t gc = (int64_t)r + caps.col_base;  // r as a column
+            if (gc >= 0 && gc < (int64_t)T.ptr.size() - 1)
+                for (int64_t q = T.ptr[(size_t)gc]; q < T.ptr[(size_t)gc + 1]; ++q) {
+                    const int x = T.all[(size_t)q];
+                    if (S.cstamp[x] == tile && !assigned[x]) ++S.inner[x];
+                }
+            // new candidates: r's columns as rows of this part
+            for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                const int cr = ci[j] - caps.col_base;  // the column's row in this block
+                if (cr >= 0 && cr < m && pid[(size_t)cr] == part && !assigned[cr] && S.cstamp[cr] != tile) {
+                    S.cstamp[cr] = tile;
+                    cand.push_back(cr);
+                    score_terms(cr);
+                }
+            }
+        };
+        add_row(seed);
+        const bool over = ucount > caps.ucap || tpad > caps.ncap;
+        while (!over && (int)rows.size() < caps.maxrows) {
+            int best = -1, best_fresh = 1 << 30;
+            long best_score = 1L << 40;
+            for (int r : cand) {
+                if (assigned[r]) continue;
+                // fewest new union rows first; among those, the row with more
+                // neighbours already in the tile (compact blobs) and more
+                // non-zeros (re-use 5.73 -> 5.80 on the cop20k_A surrogate)
+                const int len = rp[r + 1] - rp[r];
+                const long score = (long)S.fresh[r] * 64 - S.inner[r] * 16 - len;
+                if (score < best_score || (score == best_score && r < best)) {
+                    best_score = score;
+                    best_fresh = S.fresh[r];
+                    best = r;
+                }
+            }
+            if (best < 0) {
+                // no neighbour left (e.g. a diagonal or block-diagonal pattern):
+                // continue with the next unassigned row of the part
+                while (next_free < hi && assigned[P[next_free]]) ++next_free;
+                if (next_free >= hi) break;
+                best = P[next_free];
+                score_terms(best);
+                best_fresh = S.fresh[best];
+            }
+            if (ucount + best_fresh > caps.ucap ||
+                tpad + ((rp[best + 1] - rp[best] + caps.pad - 1) & ~(caps.pad - 1)) > caps.ncap)
+                break;
+            add_row(best);
+        }
+        if (caps.frontier)
+            for (int r : cand)
+                if (!assigned[r]) front.push_back(r);
+        A.grow.insert(A.grow.end(), rows.begin(), rows.end());
+        // rows by decreasing length (build_ws_plan deals them to waves in
+        // this order, so the rows of a wave have similar lengths)
+        std::sort(rows.begin(), rows.end(), [&](int a, int b) {
+            const int la = rp[a + 1] - rp[a], lb = rp[b + 1] - rp[b];
+            return la != lb ? la > lb : a < b;
+        });
+
+        TileMeta tm{};
+        tm.roff = (int)A.trows.size();
+        tm.nrows = (int)rows.size();
+        tm.noff = (int)A.padded_nnz;
+        tm.tn = (int)tnnz;
+        tm.direct = over ? 1 : 0;
+        if (over) {
+            A.ucols.resize(ubase);
+            tm.uoff = (int)ubase;
+            tm.nu = 0;
+        } else {
+            tm.uoff = (int)ubase;
+            tm.nu = ucount;
+            A.union_rows += ucount;
+            A.tiled_nnz += tnnz;
+        }
+        // tile-ordered non-zeros; every ROW segment starts at a multiple of 8
+        // entries, so the kernel's 8-wide batches of u16 / f64 LDS reads are
+        // 16-byte aligned (unaligned wide LDS reads are replayed); pads
+        // (tsrc = -1) are never summed: loops stop at the row's real length
+        int local = 0;
+        for (int r : rows) {
+            A.trows.push_back(r);
+            // packed (tile-local start, length); a direct tile's lengths are
+            // not used (the kernel reads row_ptr there)
+            const int len = rp[r + 1] - rp[r];
+            A.rbeg.push_back(over ? local : (local | (len << 16)));
+            for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                A.tsrc.push_back(j);
+                A.tlidx.push_back(over ? 0 : (uint16_t)S.upos[ci[j]]);
+                ++local;
+            }
+            while (local % 8) {
+                A.tsrc.push_back(-1);
+                A.tlidx.push_back(0);
+                ++local;
+            }
+        }
+        tm.tn = local;  // padded segment length (row ends come from rbeg / rp)
+        A.padded_nnz += local;
+        A.meta.push_back(tm);
+        ++tile;
+    }
+    return true;
+}
+
+// B's tiles appended to A (offsets shifted)
+void append_analysis(TileAnalysis &A, const TileAnalysis &B)
+{
+    const int roff = (int)A.trows.size(), uoff = (int)A.ucols.size();
+    const int64_t noff = A.padded_nnz;
+    for (TileMeta tm : B.meta) {
+        tm.roff += roff;
+        tm.uoff += uoff;
+        tm.noff += (int)noff;
+        A.meta.push_back(tm);
+    }
+    A.trows.insert(A.trows.end(), B.trows.begin(), B.trows.end());
+    A.grow.insert(A.grow.end(), B.grow.begin(), B.grow.end());
+    A.rbeg.insert(A.rbeg.end(), B.rbeg.begin(), B.rbeg.end());
+    A.ucols.insert(A.ucols.end(), B.ucols.begin(), B.ucols.end());
+    A.tsrc.insert(A.tsrc.end(), B.tsrc.begin(), B.tsrc.end());
+    A.tlidx.insert(A.tlidx.end(), B.tlidx.begin(), B.tlidx.end());
+    A.union_rows += B.union_rows;
+    A.tiled_nnz += B.tiled_nnz;
+    A.padded_nnz += B.padded_nnz;
+}
+
+}  // namespace
 
 void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A, const TileCaps &caps)
 {
     A = TileAnalysis();
-    const int ncol = std::max(n, 1);
-    std::vector<char> assigned((size_t)std::max(m, 1), 0);
-    std::vector<int> ustamp((size_t)ncol, -1);      // column in current tile union
-    std::vector<int> upos((size_t)ncol, 0);         // its position in the union
-    std::vector<int> cstamp((size_t)std::max(m, 1), -1);  // row already a candidate
-    std::vector<int64_t> probe((size_t)ncol, -1);   // column counted in a probe
-    std::vector<int> rstamp((size_t)std::max(m, 1), -1);  // row is in the current tile
-    std::vector<int> cand, rows;
-    int64_t probe_id = 0;
-    int tile = 0;
-
-    int next_free = 0;
-    std::vector<int> front;  // caps.frontier: unassigned neighbours of finished tiles, oldest first
-    size_t fhead = 0;
     // caps.part_rows / part_start: row sets tiled one after the other (a tile
     // takes rows of one part only); default one part of all rows in order
     std::vector<int> own_rows, own_start;
@@ -55,161 +284,54 @@ void analyse_tiles(int m, int n, const int *rp, const int *ci, TileAnalysis &A, 
             pid[(size_t)(*prow)[(size_t)k]] = x;
             ppos[(size_t)(*prow)[(size_t)k]] = k;
         }
-    bool stop = false;
-    for (int part = 0; part < np && !stop; ++part) {
-        const int lo = (*pst)[(size_t)part], hi = (*pst)[(size_t)part + 1];  // positions in prow
-        const int *P = prow->data();
-        A.part_tile.push_back(tile);
-        front.clear();
-        fhead = 0;
-        for (int scan = lo; scan < hi;) {
-            int seed = -1;
-            if (caps.frontier)
-                while (fhead < front.size() && seed < 0) {
-                    const int r = front[fhead++];
-                    if (!assigned[r]) seed = r;
-                }
-            if (seed < 0) {
-                while (scan < hi && assigned[P[scan]]) ++scan;
-                if (scan >= hi) break;
-                seed = P[scan];
-            }
-            if (caps.max_tiles > 0 && tile >= caps.max_tiles) {
-                stop = true;
+    ColumnRows T;
+    T.build(m, n, rp, ci);
+    std::vector<char> assigned((size_t)std::max(m, 1), 0);  // parts own disjoint rows: shared safely
+    // parts are independent (a tile takes the rows of one part; candidates
+    // are filtered by part): with several parts and no tile cap they run on
+    // threads, each with its own stamps, and are appended in part order --
+    // the result does not depend on the thread count
+    const int64_t scratch_bytes = ((int64_t)std::max(n, 1) * 16 + (int64_t)std::max(m, 1) * 16);
+    int threads = np > 1 && caps.max_tiles <= 0
+                      ? (int)std::min<int64_t>({(int64_t)np, 8, std::max<int64_t>(1, ((int64_t)1 << 31) / scratch_bytes)})
+                      : 1;
+    threads = std::max(1, std::min<int>(threads, (int)std::max(1u, std::thread::hardware_concurrency())));
+    if (analysis_threads > 0) threads = std::min(threads, analysis_threads);
+    if (threads <= 1) {
+        TileScratch S(m, n);
+        int tile = 0;
+        for (int part = 0; part < np; ++part) {
+            A.part_tile.push_back(tile);
+            if (!analyse_part(part, (*pst)[(size_t)part], (*pst)[(size_t)part + 1], prow->data(), m, rp, ci, T, pid,
+                              ppos, assigned, S, A, tile, caps))
                 break;
-            }
-            next_free = ppos[(size_t)seed] + 1;  // position after the seed in its part
-            int ucount = 0;
-            int64_t tnnz = 0, tpad = 0;  // real and row-padded non-zeros
-            rows.clear();
-            cand.clear();
-            const size_t ubase = A.ucols.size();
-            auto add_row = [&](int r) {
-                assigned[r] = 1;
-                rstamp[r] = tile;
-                rows.push_back(r);
-                tnnz += rp[r + 1] - rp[r];
-                tpad += (rp[r + 1] - rp[r] + caps.pad - 1) & ~(caps.pad - 1);
-                for (int j = rp[r]; j < rp[r + 1]; ++j) {
-                    const int c = ci[j];
-                    if (ustamp[c] != tile) {
-                        ustamp[c] = tile;
-                        upos[c] = ucount++;
-                        A.ucols.push_back(c);
-                    }
-                    const int cr = c - caps.col_base;  // the column's row in this block
-                    if (cr >= 0 && cr < m && pid[(size_t)cr] == part && !assigned[cr] && cstamp[cr] != tile) {
-                        cstamp[cr] = tile;
-                        cand.push_back(cr);
-                    }
-                }
-            };
-            add_row(seed);
-            const bool over = ucount > caps.ucap || tpad > caps.ncap;
-            while (!over && (int)rows.size() < caps.maxrows) {
-                int best = -1, best_fresh = 1 << 30;
-                long best_score = 1L << 40;
-                for (int r : cand) {
-                    if (assigned[r]) continue;
-                    ++probe_id;
-                    int fresh = 0, inner = 0;
-                    for (int j = rp[r]; j < rp[r + 1]; ++j) {
-                        const int c = ci[j];
-                        const int cr = c - caps.col_base;
-                        if (cr >= 0 && cr < m && rstamp[cr] == tile) ++inner;
-                        if (ustamp[c] != tile && probe[c] != probe_id) {
-                            probe[c] = probe_id;
-                            ++fresh;
-                        }
-                    }
-                    // fewest new union rows first; among those, the row with more
-                    // neighbours already in the tile (compact blobs) and more
-                    // non-zeros (re-use 5.73 -> 5.80 on the cop20k_A surrogate)
-                    const int len = rp[r + 1] - rp[r];
-                    const long score = (long)fresh * 64 - inner * 16 - len;
-                    if (score < best_score || (score == best_score && r < best)) {
-                        best_score = score;
-                        best_fresh = fresh;
-                        best = r;
-                    }
-                }
-                if (best < 0) {
-                    // no neighbour left (e.g. a diagonal or block-diagonal pattern):
-                    // continue with the next unassigned row of the part
-                    while (next_free < hi && assigned[P[next_free]]) ++next_free;
-                    if (next_free >= hi) break;
-                    best = P[next_free];
-                    ++probe_id;
-                    best_fresh = 0;
-                    for (int j = rp[best]; j < rp[best + 1]; ++j) {
-                        const int c = ci[j];
-                        if (ustamp[c] != tile && probe[c] != probe_id) {
-                            probe[c] = probe_id;
-                            ++best_fresh;
-                        }
-                    }
-                }
-                if (ucount + best_fresh > caps.ucap ||
-                    tpad + ((rp[best + 1] - rp[best] + caps.pad - 1) & ~(caps.pad - 1)) > caps.ncap)
-                    break;
-                add_row(best);
-            }
-            if (caps.frontier)
-                for (int r : cand)
-                    if (!assigned[r]) front.push_back(r);
-            A.grow.insert(A.grow.end(), rows.begin(), rows.end());
-            // rows by decreasing length (build_ws_plan deals them to waves in
-            // this order, so the rows of a wave have similar lengths)
-            std::sort(rows.begin(), rows.end(), [&](int a, int b) {
-                const int la = rp[a + 1] - rp[a], lb = rp[b + 1] - rp[b];
-                return la != lb ? la > lb : a < b;
-            });
-
-            TileMeta tm{};
-            tm.roff = (int)A.trows.size();
-            tm.nrows = (int)rows.size();
-            tm.noff = (int)A.padded_nnz;
-            tm.tn = (int)tnnz;
-            tm.direct = over ? 1 : 0;
-            if (over) {
-                A.ucols.resize(ubase);
-                tm.uoff = (int)ubase;
-                tm.nu = 0;
-            } else {
-                tm.uoff = (int)ubase;
-                tm.nu = ucount;
-                A.union_rows += ucount;
-                A.tiled_nnz += tnnz;
-            }
-            // tile-ordered non-zeros; every ROW segment starts at a multiple of 8
-            // entries, so the kernel's 8-wide batches of u16 / f64 LDS reads are
-            // 16-byte aligned (unaligned wide LDS reads are replayed); pads
-            // (tsrc = -1) are never summed: loops stop at the row's real length
-            int local = 0;
-            for (int r : rows) {
-                A.trows.push_back(r);
-                // packed (tile-local start, length); a direct tile's lengths are
-                // not used (the kernel reads row_ptr there)
-                const int len = rp[r + 1] - rp[r];
-                A.rbeg.push_back(over ? local : (local | (len << 16)));
-                for (int j = rp[r]; j < rp[r + 1]; ++j) {
-                    A.tsrc.push_back(j);
-                    A.tlidx.push_back(over ? 0 : (uint16_t)upos[ci[j]]);
-                    ++local;
-                }
-                while (local % 8) {
-                    A.tsrc.push_back(-1);
-                    A.tlidx.push_back(0);
-                    ++local;
-                }
-            }
-            tm.tn = local;  // padded segment length (row ends come from rbeg / rp)
-            A.padded_nnz += local;
-            A.meta.push_back(tm);
-            ++tile;
         }
+        while ((int)A.part_tile.size() <= np) A.part_tile.push_back(tile);
+        return;
     }
-    while ((int)A.part_tile.size() <= np) A.part_tile.push_back(tile);
+    std::vector<TileAnalysis> out((size_t)np);
+    std::atomic<int> next{0};
+    auto worker = [&]() {
+        TileScratch S(m, n);
+        for (int part; (part = next++) < np;) {
+            int tile = 0;
+            analyse_part(part, (*pst)[(size_t)part], (*pst)[(size_t)part + 1], prow->data(), m, rp, ci, T, pid, ppos,
+                         assigned, S, out[(size_t)part], tile, caps);
+            // stamps are per tile id: the next part on this thread starts clean
+            std::fill(S.ustamp.begin(), S.ustamp.end(), -1);
+            std::fill(S.cstamp.begin(), S.cstamp.end(), -1);
+            std::fill(S.rstamp.begin(), S.rstamp.end(), -1);
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; ++t) pool.emplace_back(worker);
+    worker();
+    for (auto &t : pool) t.join();
+    for (int part = 0; part < np; ++part) {
+        A.part_tile.push_back((int)A.meta.size());
+        append_analysis(A, out[(size_t)part]);
+    }
+    A.part_tile.push_back((int)A.meta.size());
 }
 
 // ---------------------------------------------------------------------------

@@ -96,8 +96,11 @@ struct TileCaps {
     std::vector<int> part_rows, part_start;
     int xcd_blocks = 32;           // k_rows_ws blocks per XCD (MI355X: 256 CUs / 8 XCDs)
 };
+// Independent parts are analysed on up to 8 threads; analysis_threads > 0
+// caps that for analyses run on the calling thread (smfv_set_analysis_threads).
 void analyse_tiles(int m, int n, const int *row_ptr, const int *col_idx, TileAnalysis &out,
                    const TileCaps &caps = TileCaps());
+extern thread_local int analysis_threads;
 
 struct WsPlan {
     int ntiles = 0;

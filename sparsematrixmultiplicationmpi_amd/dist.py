@@ -123,19 +123,28 @@ class DistPlan:
     where it pays -- plus the exchange buffers and schedule.
 
     rowpart=True: A holds only this rank's rows of the RowWise partition of
-    an m-row matrix (smfv_dist_plan_create_rowpart; `m` required)."""
+    an m-row matrix (smfv_dist_plan_create_rowpart; `m` required).
 
-    def __init__(self, comm: Communicator, variant: int, A: DeviceCSR, K: int, to_all: bool,
+    comm=None with rank=(r, p): the plan of rank r of p alone, no
+    communicator (smfv_dist_plan_create_rank): run_local() computes what that
+    rank of the reference's variant computes, into Y (ROWWISE) or the plan's
+    exchange buffer (exchange_buffer()); exchange() is refused."""
+
+    def __init__(self, comm: Communicator | None, variant: int, A: DeviceCSR, K: int, to_all: bool,
                  root: int = 0, tiles: str = "auto", rowpart: bool = False, m: int | None = None,
-                 stream=None):
+                 stream=None, rank: tuple[int, int] | None = None, fma: bool = False):
         self.comm, self.variant, self.A, self.K = comm, Variant(variant), A, K
         self.mode = TO_ALL if to_all else TO_ROOT
         self.root = root
         self.m = A.m if not rowpart else int(m)
-        flags = {"auto": 0, "off": 1, "force": 2}[tiles]
+        flags = {"auto": 0, "off": 1, "force": 2}[tiles] | (4 if fma else 0)
         ip = POINTER(c_int)
         self._h = c_void_p()
-        if rowpart:
+        if comm is None:
+            r, p = rank
+            call("smfv_dist_plan_create_rank", byref(self._h), int(p), int(r), int(variant), self.mode, root, A.m,
+                 A.n, A.nnz, A.h_row_ptr.ctypes.data_as(ip), A.h_col_idx.ctypes.data_as(ip), K, flags)
+        elif rowpart:
             call("smfv_dist_plan_create_rowpart", byref(self._h), comm.handle, self.mode, root, self.m, A.n,
                  A.h_row_ptr.ctypes.data_as(ip), A.h_col_idx.ctypes.data_as(ip), K, flags)
         else:
@@ -171,6 +180,18 @@ class DistPlan:
         call("smfv_dist_plan_exchange", self._h, Y.data_ptr(), stream_handle(stream))
         return Y
 
+    def exchange_buffer(self) -> torch.Tensor | None:
+        """The plan's exchange buffer as a (device) tensor view: rank-major
+        COLUMNWISE panels / NONZERO compact row blocks, laid out as
+        exchange_plan's offset / count say; None for ROWWISE (Y itself)."""
+        ptr, n = ctypes.POINTER(ctypes.c_double)(), c_int64(0)
+        call("smfv_dist_plan_exchange_buffer", self._h, byref(ptr), byref(n))
+        if not n.value:
+            return None
+        addr = ctypes.cast(ptr, c_void_p).value
+        # a non-owning view of the plan's device buffer (the plan outlives it)
+        return _device_view(addr, n.value, self.A.device, owner=self)
+
     def stats(self) -> dict:
         from .engine import PLAN_STATS
         out = (ctypes.c_double * PLAN_STATS)()
@@ -186,6 +207,17 @@ class DistPlan:
                 self._h = c_void_p()
         except Exception:
             pass
+
+
+def _device_view(addr: int, count: int, device: torch.device, owner) -> torch.Tensor:
+    """A float64 tensor over `count` doubles of device memory at `addr` that
+    the library owns (kept alive by `owner`)."""
+    class _Holder:
+        def __init__(self):
+            self.owner = owner
+            self.__cuda_array_interface__ = {"shape": (count,), "typestr": "<f8", "data": (addr, False),
+                                             "version": 3, "strides": None, "stream": None}
+    return torch.as_tensor(_Holder(), device=device)
 
 
 def dist_spmm(comm: Communicator, variant: int, A: DeviceCSR, X: torch.Tensor, to_all: bool = False,

@@ -53,8 +53,11 @@ class DeviceCSR:
 
     spmm() keeps one plan per (variant, K) on the matrix (analysed once).  A
     tiled plan computes with a snapshot of the values taken when it was bound
-    (include/smfv.h, values contract): after changing `values` in place call
-    values_changed(), which re-binds every cached plan."""
+    (include/smfv.h, values contract).  The cached plans re-bind by
+    themselves when `values` has changed since their bind -- a new tensor, or
+    an in-place change (torch's version counter of the tensor) -- and
+    values_changed() re-binds them explicitly (e.g. after a write torch did
+    not see, such as a kernel of another library)."""
 
     def __init__(self, A: SparseMatrix, device: torch.device | None = None):
         device = device or _require_device()
@@ -81,7 +84,14 @@ class DeviceCSR:
         p = self._plans.get(key)
         if p is None:
             p = self._plans[key] = SpmmPlan(variant, self, K, stream=stream)
+        elif p.bound_version != self.values_version():
+            p.bind_values(stream)  # values changed since the bind: snapshot them again
         return p
+
+    def values_version(self) -> tuple[int, int]:
+        """(address, torch version counter) of `values`: changes with every
+        in-place write torch performs and with a new tensor."""
+        return self.values.data_ptr(), self.values._version
 
     def values_changed(self, stream: torch.cuda.Stream | None = None) -> None:
         """Re-bind every cached plan after `values` changed in place."""
@@ -157,6 +167,7 @@ class SpmmPlan:
     def bind_values(self, stream: torch.cuda.Stream | None = None) -> None:
         """(Re)bind a tiled plan to A's current device values (after they change)."""
         call("smfv_plan_bind_values", self._plan, self.A.values.data_ptr(), stream_handle(stream))
+        self.bound_version = self.A.values_version()
 
     def stats(self) -> dict:
         out = (ctypes.c_double * PLAN_STATS)()

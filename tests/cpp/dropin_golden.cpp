@@ -13,8 +13,12 @@
 // Prints "DROPIN GOLDEN OK" and exits 0, or names the failure and exits 1.
 #include <mpi.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <thread>
+#include <utility>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -52,6 +56,18 @@ static void expect(bool ok, const std::string &what)
         std::printf("FAIL %s\n", what.c_str());
         ++failures;
     }
+}
+
+// the reference's loop (SC/SparseMatrixFatVectorMultiply.cpp:17-27): per
+// row, non-zeros in CSR order, y += a * x with a separate multiply and add
+// (this file is built with -ffp-contract=off)
+static FatVector host_spmm(const SparseMatrix &A, const FatVector &X, int K)
+{
+    FatVector Y((size_t)A.numRows, std::vector<double>((size_t)K, 0.0));
+    for (int i = 0; i < A.numRows; ++i)
+        for (int j = A.rowPtr[i]; j < A.rowPtr[i + 1]; ++j)
+            for (int k = 0; k < K; ++k) Y[i][k] += A.values[j] * X[A.colIndices[j]][k];
+    return Y;
 }
 
 static bool same_bits(const FatVector &a, const FatVector &b)
@@ -131,6 +147,41 @@ int main(int argc, char **argv)
         if (same) std::printf("note: r0=%d y2=%.17g yseq=%.17g x=%.17g d=%.17g\n", r0, Y2[r0][0], Yseq[r0][0],
                               X[A.colIndices[0]][0], dd);
         expect(!same || X[A.colIndices[0]][0] == 0.0, "device compare sees the change");
+    }
+    // (r3) resident inputs changed IN PLACE (same objects, same addresses)
+    // after smfvDistributeInputs: the call sees the new values and X
+    if (m > 0 && !A.values.empty() && K > 0) {
+        FatVector X2 = X;
+        smfvDistributeInputs(A, X2, K);
+        expect(same_bits(sparseMatrixFatVectorMultiplyRowWise(A, X2, K), host_spmm(A, X2, K)), "resident (unchanged)");
+        A.values[A.values.size() / 2] = -3.25;
+        X2[A.colIndices[0]][K - 1] += 7.0;
+        expect(same_bits(sparseMatrixFatVectorMultiplyRowWise(A, X2, K), host_spmm(A, X2, K)),
+               "resident inputs edited in place are re-uploaded");
+        expect(same_bits(sparseMatrixFatVectorMultiply(A, X2, K), host_spmm(A, X2, K)), "resident, sequential");
+        smfvReleaseInputs();
+    }
+    // (r3) another pattern with the same sizes: a plan-cache key match (forced
+    // by SMFV_TEST_PLAN_KEY_BITS=0 in the test) must not run the first
+    // pattern's plan
+    if (m > 1 && n > 1 && nnz > 0 && K > 0) {
+        SparseMatrix B = A;
+        for (int i = 0; i < m; ++i) {  // every column shifted by one, rows re-sorted by (col, value)
+            std::vector<std::pair<int, double>> row;
+            for (int j = A.rowPtr[i]; j < A.rowPtr[i + 1]; ++j) row.push_back({(A.colIndices[j] + 1) % n, A.values[j]});
+            std::sort(row.begin(), row.end());
+            for (int j = A.rowPtr[i], q = 0; j < A.rowPtr[i + 1]; ++j, ++q) {
+                B.colIndices[j] = row[q].first;
+                B.values[j] = row[q].second;
+            }
+        }
+        for (int pass = 0; pass < 3; ++pass) {  // the third pass may run a background-built tiled plan
+            expect(same_bits(sparseMatrixFatVectorMultiplyRowWise(B, X, K), host_spmm(B, X, K)),
+                   "second pattern, same sizes (RowWise)");
+            expect(same_bits(sparseMatrixFatVectorMultiplyRowWise(A, X, K), host_spmm(A, X, K)),
+                   "first pattern again (RowWise)");
+            if (pass == 1) std::this_thread::sleep_for(std::chrono::milliseconds(500));
+        }
     }
     std::printf(failures ? "DROPIN GOLDEN FAILED (%d)\n" : "DROPIN GOLDEN OK%.0d\n", failures);
     MPI_Finalize();

@@ -42,3 +42,21 @@ def test_every_config_is_a_baseline_workload():
     assert {"cop20k", "pow10m", "syn80m"} <= kinds
     assert bench.CONFIGS["cop20k_k32"] == ("cop20k", 32, "ROWWISE")
     assert bench.CONFIGS["pow10m_k32"][2] == "NONZERO"
+
+
+def test_phase_deadline_prints_a_line_and_exits_4():
+    """A multi-GPU phase that never ends (e.g. a hung RCCL call on a first
+    8-GPU run) becomes one diagnostic JSON line and exit status 4."""
+    import subprocess
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "d = bench.Deadline(0.5, 3, 8, 'm'); d.enter('fast'); d.enter('stuck collective'); "
+            "time.sleep(30)") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 4, (r.returncode, r.stderr[-500:])
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["value"] is None and "stuck collective" in line["error"] and line["rank"] == 3
+    # a cancelled deadline never fires
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "d = bench.Deadline(0.3, 0, 1, 'm'); d.enter('x'); d.cancel(); time.sleep(1); print('done')") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip() == "done"

@@ -16,9 +16,16 @@ MPIEXEC = "/opt/conda/bin/mpiexec"
 MAIN = os.path.join(ROOT, "sparsematrixmultiplicationmpi_amd", "smfv_main")
 
 
-def run_main(args, n=1, timeout=180):
+def run_main(args, n=1, timeout=180, env=None):
     return subprocess.run([MPIEXEC, "-launcher", "fork", "-n", str(n), MAIN] + args,
-                          capture_output=True, text=True, timeout=timeout)
+                          capture_output=True, text=True, timeout=timeout,
+                          env=None if env is None else dict(os.environ, **env))
+
+
+def value(out, label):
+    m = re.search(rf"^{re.escape(label)}: ([0-9.eE+-]+)$", out, re.M)
+    assert m, label
+    return float(m.group(1))
 
 
 @pytest.mark.gpu
@@ -39,7 +46,10 @@ def test_cli_stdout_contract(tmp_path):
         assert f"{name}: Results are the same!" in out  # checked on the device (smfvCompareWithReference)
     # (r2) device-resident input distribution, timed on its own line
     assert re.search(r"^Input distribution time: [0-9.eE+-]+$", out, re.M)
-    assert re.search(r"^Plan setup time: [0-9.eE+-]+$", out, re.M)
+    # (r3) no per-variant warm-up: each variant's line is its first call
+    # (SC/main.cpp:161-163); only the device start-up is done before, untimed
+    assert "Plan setup time" not in out
+    assert re.search(r"^Device init time: [0-9.eE+-]+$", out, re.M)
     # the PETSc block's analogue (SC/main.cpp:352,388 line shapes)
     assert re.search(r"^rocSPARSE Execution time: [0-9.eE+-]+$", out, re.M)
     assert "rocSPARSE: Results are the same!" in out
@@ -51,3 +61,34 @@ def test_cli_usage_error():
     r = run_main(["8"])  # wrong argc -> usage + MPI_Abort (SC/main.cpp:23-30), no GPU touched
     assert r.returncode != 0
     assert "Usage:" in r.stderr
+
+
+@pytest.mark.gpu
+def test_cli_stage_timing_lines(tmp_path):
+    """SMFV_TIMING=1: every call prints its stage times in the reference's
+    debug-line format ("Row-wise Average Computation Time: t" / "Average
+    Communication Time", SC/...RowWise.cpp:96-108, scraped by
+    SC/scripts/get_csv_all.sh:25-44 / get_csv_debug.sh, which also reads the
+    "Broadcast time" line) plus host preparation, H2D, D2H and rebuild; the
+    stages follow each other, so they add up to the call's execution time
+    (within 10 %)."""
+    A = smfv.gen_fem27(20000, 24, 24, 0.8, 6)
+    mtx = tmp_path / "b.mtx"
+    smfv.writeMatrixMarketFile(str(mtx), A, symmetric=True)
+    r = run_main(["32", str(mtx)], env={"SMFV_TIMING": "1"})
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = r.stdout
+    assert re.search(r"^Broadcast time: [0-9.eE+-]+$", out, re.M)
+    for label, name in (("Serial Algo", "Serial Algo"), ("Row-wise", "Row-wise"), ("Column-wise", "Column-wise"),
+                        ("Non-zero Elements", "Non-zero elements")):
+        stages = [value(out, f"{name} {s}") for s in
+                  ("Average Computation Time", "Average Communication Time", "Host Preparation Time",
+                   "Host-to-Device Time", "Device-to-Host Time", "FatVector Rebuild Time")]
+        total = value(out, f"{label} Execution time")
+        assert all(s >= 0 for s in stages) and stages[0] > 0 and stages[4] > 0, (name, stages)
+        assert abs(sum(stages) - total) <= 0.10 * total, (name, stages, total)
+    # the scrapers' field positions (awk '{print $5}' / '{print $6}')
+    line = next(x for x in out.splitlines() if x.startswith("Row-wise Average Computation Time"))
+    float(line.split()[4])
+    line = next(x for x in out.splitlines() if x.startswith("Non-zero elements Average Communication Time"))
+    float(line.split()[5])

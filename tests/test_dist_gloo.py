@@ -191,3 +191,87 @@ def test_gloo_rowpart(p, m):
     for rank, ok, info in res:
         assert ok, (p, m, rank, info)
         assert info is (m % p == 0)  # equal blocks -> the single ncclAllGather op
+
+
+def _golden_worker(rank, p, port, name, q):
+    """The reference's own degenerate case at p = 8 (pat4x6_k3: K < p for
+    ColumnWise, m < p for RowWise, nnz < p for NonZeroElement): every rank
+    takes its part from the native plan, computes it with the oracle, and
+    the native schedule, replayed over gloo, must give the reference's own
+    results -- Y_seq bit for bit (RowWise / ColumnWise), the reference's
+    NonZeroElement output at p (Y_nnz_p{p}) within 1e-12 x sum|a||x| --
+    for every variant, on every rank (TO_ALL) or the root (TO_ROOT)."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=p)
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import sparsematrixmultiplicationmpi_amd as smfv
+        from sparsematrixmultiplicationmpi_amd.dist import TO_ALL, exchange_ops, exchange_plan
+        from conftest import load_golden
+        from oracle import oracle
+
+        g = load_golden(name)
+        A = smfv.SparseMatrix(np.asarray(g["values"], np.float64), np.asarray(g["col_idx"], np.int32),
+                              np.asarray(g["row_ptr"], np.int32), int(g["m"]), int(g["n"]))
+        X = np.ascontiguousarray(g["X"], np.float64)
+        K = X.shape[1]
+        m, nnz = A.numRows, A.nnz
+        absY = oracle.spmm("sequential", A.rowPtr, A.colIndices, np.abs(A.values), np.abs(X))
+        results = []
+        for variant in (1, 2, 3):
+            first, last, off, cnt = exchange_plan(variant, m, nnz, A.rowPtr, K, p)
+            for mode in (0, 1):
+                root = p - 1
+                mine = _local_part(variant, A, X, first[rank], last[rank], rank, p)
+                assert mine.size == cnt[rank]
+                xbuf = torch.full((max(int((off + cnt).max()), 1),), float("nan"), dtype=torch.float64)
+                xbuf[off[rank]: off[rank] + cnt[rank]] = torch.from_numpy(mine)
+                run_ops(exchange_ops(variant, mode, root, m, nnz, A.rowPtr, K, p, rank), xbuf, rank, p)
+                if mode != TO_ALL and rank != root:
+                    continue
+                xb = xbuf.numpy()
+                Y = np.zeros((m, K))
+                if variant == 1:
+                    Y = xb[:m * K].reshape(m, K)
+                elif variant == 2:
+                    for r in range(p):
+                        kc = last[r] - first[r] + 1
+                        if kc > 0:
+                            Y[:, first[r]:last[r] + 1] = xb[off[r]: off[r] + m * kc].reshape(m, kc)
+                else:
+                    seen = np.zeros(m, bool)
+                    for r in range(p):
+                        nr = last[r] - first[r] + 1
+                        if nr <= 0:
+                            continue
+                        blk = xb[off[r]: off[r] + nr * K].reshape(nr, K)
+                        rows = slice(first[r], last[r] + 1)
+                        Y[rows] = np.where(seen[rows, None], Y[rows] + blk, blk)
+                        seen[rows] = True
+                if variant == 3:
+                    err = float(np.max(np.abs(Y - g[f"Y_nnz_p{p}"]) / np.maximum(absY, 1e-300)))
+                    results.append((variant, mode, err <= 1e-12, err))
+                else:
+                    results.append((variant, mode, bool(np.array_equal(Y.view(np.uint64), g["Y_seq"].view(np.uint64))),
+                                    None))
+        q.put((rank, all(r[2] for r in results), results))
+        dist.destroy_process_group()
+    except Exception as e:  # surface worker failures
+        q.put((rank, False, repr(e)))
+
+
+def test_gloo_reference_degenerate_p8():
+    """pat4x6_k3 at p = 8 over gloo: all three variants, both modes, root 7."""
+    p = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_golden_worker, args=(r, p, port, "pat4x6_k3", q)) for r in range(p)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=300) for _ in range(p)]
+    for pr in procs:
+        pr.join(timeout=60)
+    for rank, ok, info in res:
+        assert ok, (rank, info)

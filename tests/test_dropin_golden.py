@@ -3,7 +3,10 @@ SC/SparseMatrixFatVectorMultiply*.h) pinned to the golden fixtures the
 reference itself produced (tests/golden): a compiled C++ program
 (tests/cpp/dropin_golden.cpp -> smfv_dropin_golden) calls the four functions,
 the device-resident path (smfvDistributeInputs) and the device-side check,
-and compares bit for bit (NonZeroElement within 1e-12 x sum|a||x|)."""
+and compares bit for bit (NonZeroElement within 1e-12 x sum|a||x|).  (r3)
+It also edits resident inputs in place (the call must see the edit) and
+runs a second pattern of the same sizes, once with the plan-cache key
+forced to collide (the stored pattern must be compared on a key match)."""
 import os
 import subprocess
 
@@ -31,7 +34,11 @@ def test_dropin_golden(tmp_path, name):
     smfv.inputs.write_csr_bin(str(tmp_path / "a.bin"), A)
     smfv.inputs.write_dense_bin(str(tmp_path / "x.bin"), g["X"])
     smfv.inputs.write_dense_bin(str(tmp_path / "y.bin"), g["Y_seq"])
-    r = subprocess.run([MPIEXEC, "-launcher", "fork", "-n", "1", PROG, str(tmp_path / "a.bin"),
-                        str(tmp_path / "x.bin"), str(tmp_path / "y.bin")],
-                       capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0 and "DROPIN GOLDEN OK" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])
+    # SMFV_TEST_PLAN_KEY_BITS=0: every pattern of equal sizes has the same plan
+    # key, so the program's second pattern hits the first one's cache entry
+    # unless the stored pattern is compared (it is: the result must be B's)
+    for env in ({}, {"SMFV_TEST_PLAN_KEY_BITS": "0"}):
+        r = subprocess.run([MPIEXEC, "-launcher", "fork", "-n", "1", PROG, str(tmp_path / "a.bin"),
+                            str(tmp_path / "x.bin"), str(tmp_path / "y.bin")],
+                           capture_output=True, text=True, timeout=120, env=dict(os.environ, **env))
+        assert r.returncode == 0 and "DROPIN GOLDEN OK" in r.stdout, (env, r.stdout[-3000:], r.stderr[-3000:])

@@ -488,9 +488,10 @@ def test_plan_bind_on_other_stream(gpu):
 
 
 def test_plan_values_snapshot_contract(gpu):
-    """ADVICE r1 / include/smfv.h values contract: a tiled plan computes with
-    the values bound last -- for the tiles AND the direct rows (no mixing) --
-    until values_changed() re-binds; then it sees the new values."""
+    """ADVICE r1 / include/smfv.h values contract: an explicit tiled plan
+    computes with the values bound last -- for the tiles AND the direct rows
+    (no mixing) -- until values_changed() re-binds; then it sees the new
+    values.  The matrix's cached plans (spmm) re-bind on their own."""
     A = _forced_plan_matrix(47)
     K = 32
     X = np.random.default_rng(47).uniform(-1, 1, (A.numCols, K))
@@ -508,6 +509,9 @@ def test_plan_values_snapshot_contract(gpu):
     forced.run(dX, Y)
     torch.cuda.synchronize()
     assert np.array_equal(bits(Y.cpu().numpy()), bits(Y_old))  # the bound snapshot, all rows
+    # the matrix's cached plan (spmm) re-binds by itself after an
+    # in-place change torch has seen (the tensor's version counter moved)
+    assert np.array_equal(bits(smfv.spmm(smfv.Variant.ROWWISE, dA, dX).cpu().numpy()), bits(Y_new))
     dA.values_changed()
     forced.run(dX, Y)
     torch.cuda.synchronize()
