@@ -55,7 +55,8 @@ def metric_for(config: str, K: int, variant: str) -> str:
     if config == "cop20k_k32" and variant == "ROWWISE":
         return HEADLINE_METRIC
     what = {"cop20k": "cop20k_A", "pow10m": "synthetic 10M x 10M power-law", "syn80m": "synthetic 80M x 80M",
-            "cop20k_perm": "cop20k_A (randomly permuted)"}[CONFIGS[config][0]]
+            "cop20k_perm": "cop20k_A (randomly permuted)",
+            "cop20k_irr": "cop20k_A (irregular surrogate)"}[CONFIGS[config][0]]
     return f"effective GFLOP/s + achieved HBM GB/s, {what} × K={K}, {variant}"
 
 
@@ -73,6 +74,9 @@ CONFIGS = {
     "pow10m_k1": ("pow10m", 1, "SEQUENTIAL"),  # K = 1 on power-law rows (k_spmv_stream long rows)
     # the headline matrix under a random symmetric permutation (ordering robustness)
     "cop20k_perm_k32": ("cop20k_perm", 32, "ROWWISE"),
+    # a second cop20k_A stand-in with the same m and nnz, unstructured (k-NN of
+    # clustered 3-D points, row degrees 4..85): the plan on an irregular pattern
+    "cop20kirr_k32": ("cop20k_irr", 32, "ROWWISE"),
     # config 5: 80M x 80M, 16 nnz/row, row-partitioned over the ranks + RCCL all-gather
     "syn80m_k32": ("syn80m", 32, "ROWWISE"),
 }
@@ -128,6 +132,10 @@ def build_matrix(kind: str, mtx: str | None):
         perm = np.random.default_rng(2024).permutation(A.numRows)
         return (inputs.permute_symmetric(A, perm),
                 "cop20k_A surrogate under a random symmetric permutation (seed 2024)")
+    if kind == "cop20k_irr":
+        return (inputs.cop20k_irregular_surrogate(),
+                "cop20k_A irregular surrogate (knn3d: clustered 3-D points, variable-k nearest neighbours, "
+                "symmetrised, Morton order; m=121192, degrees 4..85)")
     if kind == "pow10m":
         m = 10_000_000
         return (inputs.gen_random_rows(m, m, 16.0, 2.0, 4096, 42),
@@ -745,7 +753,7 @@ def main() -> None:
         return
     mode = args.mode or ("decomposed" if world > 1 else "replicas")
     fallback = None
-    if mode == "decomposed" and kind in ("cop20k", "cop20k_perm"):
+    if mode == "decomposed" and kind in ("cop20k", "cop20k_perm", "cop20k_irr"):
         fallback = bench_decomposed(args, world, rank, local, kind, K, variant)
         if fallback is None:
             return
@@ -753,7 +761,7 @@ def main() -> None:
 
     A, label = build_matrix(kind, args.mtx)
     m, n, nnz = A.numRows, A.numCols, A.nnz
-    cop = kind in ("cop20k", "cop20k_perm")
+    cop = kind in ("cop20k", "cop20k_perm", "cop20k_irr")
 
     # CPU baseline first: rank 0 at N = 1, before anything touches the GPU
     cpu = None

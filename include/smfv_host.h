@@ -70,6 +70,17 @@ SMFV_API int smfv_dense_write_bin(const char *path, int64_t rows, int64_t cols, 
 SMFV_API int smfv_gen_fem27(int m, int nx, int ny, double keep, uint64_t seed, int64_t *nnz,
                             int **row_ptr, int **col_idx, double **values);
 
+/* Irregular FEM-like surrogate (a second stand-in for cop20k_A with the
+ * same m and nnz but no stencil regularity): m points in the unit cube, 70 %
+ * uniform and 30 % in Gaussian clusters, each joined to its k_i nearest
+ * points (k_i in [3, 48], log-graded along the cube's diagonal, times a
+ * scale bisected so that nnz is
+ * as close to target_nnz as the scale allows), symmetrised, diagonal
+ * added, rows numbered in Morton order of the points.  Row degrees spread
+ * ~5..80; values symmetric as smfv_gen_fem27. */
+SMFV_API int smfv_gen_knn3d(int m, int64_t target_nnz, uint64_t seed, int64_t *nnz, int **row_ptr, int **col_idx,
+                            double **values);
+
 /* Rows [row_begin, row_end) of an m x n matrix with row lengths drawn from
  * a truncated power law (P(L >= x) ~ x^(1-alpha), cap `cap`) scaled to the
  * requested mean, columns uniform and distinct per row, sorted; values in

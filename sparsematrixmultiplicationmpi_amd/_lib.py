@@ -128,6 +128,7 @@ _SIGS = {
     "smfv_dense_write_bin": (c_int, [c_char_p, c_int64, c_int64, _PD]),
     "smfv_gen_fem27": (c_int, [c_int, c_int, c_int, c_double, c_uint64, _PI64, POINTER(_PI),
                                POINTER(_PI), POINTER(_PD)]),
+    "smfv_gen_knn3d": (c_int, [c_int, c_int64, c_uint64, _PI64, POINTER(_PI), POINTER(_PI), POINTER(_PD)]),
     "smfv_gen_random_rows": (c_int, [c_int64, c_int64, c_int64, c_int64, c_double, c_double,
                                      c_int, c_uint64, _PI64, POINTER(_PI), POINTER(_PI),
                                      POINTER(_PD)]),

@@ -449,6 +449,182 @@ SMFV_API int smfv_dense_write_bin(const char *path, int64_t rows, int64_t cols, 
 // ---------------------------------------------------------------------------
 // fem27: symmetric 27-point-stencil surrogate
 // ---------------------------------------------------------------------------
+// Irregular FEM-like surrogate: m points in the unit cube, 70 % uniform and
+// 30 % in 48 Gaussian clusters (so the neighbour distance varies ~5x), each
+// joined to its k_i nearest points (see below)
+// scale s, the graph symmetrised (union) plus the diagonal, rows numbered in
+// Morton (Z) order of the points -- a mesh-like numbering with locality but
+// no stencil regularity.  s is bisected so that nnz lands on target_nnz.
+// Row degrees spread from ~4 to ~80 (k_i in [3, 48] x s, log-graded along
+// the cube's diagonal with noise, at most 64 out-neighbours).  Values as fem27 (symmetric,
+// off-diagonal in [-1, 1), diagonal in [1, 2)).
+SMFV_API int smfv_gen_knn3d(int m, int64_t target_nnz, uint64_t seed, int64_t *out_nnz, int **out_rp, int **out_ci,
+                            double **out_va)
+{
+    SMFV_REQUIRE(m >= 2 && target_nnz >= m && out_nnz && out_rp && out_ci && out_va, "bad knn3d parameters");
+    constexpr int KMAX = 64, NCL = 48;
+    // points (hash-based, independent of the thread count)
+    std::vector<double> P((size_t)m * 3);
+    std::vector<double> cen(NCL * 3);
+    for (int c = 0; c < NCL * 3; ++c) cen[c] = 0.1 + 0.8 * u01(hash3(seed, 0xC1u, (uint64_t)c));
+    auto gauss = [](uint64_t h1, uint64_t h2) {
+        const double u = std::max(u01(h1), 1e-300), v = u01(h2);
+        return std::sqrt(-2.0 * std::log(u)) * std::cos(6.283185307179586 * v);
+    };
+    parallel_rows(0, m, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            const uint64_t h = hash3(seed, 0xA0u, (uint64_t)i);
+            if (u01(h) < 0.7) {
+                for (int d = 0; d < 3; ++d) P[(size_t)i * 3 + d] = u01(hash3(seed, 0xB0u + d, (uint64_t)i));
+            } else {
+                const int c = (int)(splitmix64(h) % NCL);
+                for (int d = 0; d < 3; ++d) {
+                    double x = cen[c * 3 + d] + 0.035 * gauss(hash3(seed, 0xD0u + d, (uint64_t)i),
+                                                              hash3(seed, 0xE0u + d, (uint64_t)i));
+                    P[(size_t)i * 3 + d] = std::min(1.0 - 1e-9, std::max(0.0, x));
+                }
+            }
+        }
+    });
+    // Morton order
+    auto morton = [&](int64_t i) {
+        uint64_t code = 0;
+        for (int d = 0; d < 3; ++d) {
+            uint64_t q = (uint64_t)(P[(size_t)i * 3 + d] * 2097152.0);  // 21 bits
+            for (int b = 0; b < 21; ++b) code |= ((q >> b) & 1ull) << (3 * b + d);
+        }
+        return code;
+    };
+    std::vector<std::pair<uint64_t, int>> ord((size_t)m);
+    for (int i = 0; i < m; ++i) ord[i] = {morton(i), i};
+    std::sort(ord.begin(), ord.end());
+    {
+        std::vector<double> Q((size_t)m * 3);
+        for (int i = 0; i < m; ++i)
+            for (int d = 0; d < 3; ++d) Q[(size_t)i * 3 + d] = P[(size_t)ord[i].second * 3 + d];
+        P.swap(Q);
+    }
+    // grid buckets (about two points per cell)
+    const int G = std::max(1, (int)std::cbrt((double)m / 2.0));
+    std::vector<int> cstart((size_t)G * G * G + 1, 0), cell((size_t)m), cpts((size_t)m);
+    auto cell_of = [&](int i, int d) { return std::min(G - 1, (int)(P[(size_t)i * 3 + d] * G)); };
+    for (int i = 0; i < m; ++i) {
+        cell[i] = (cell_of(i, 2) * G + cell_of(i, 1)) * G + cell_of(i, 0);
+        ++cstart[(size_t)cell[i] + 1];
+    }
+    for (size_t c = 0; c + 1 < cstart.size(); ++c) cstart[c + 1] += cstart[c];
+    {
+        std::vector<int> fill(cstart.begin(), cstart.end() - 1);
+        for (int i = 0; i < m; ++i) cpts[(size_t)fill[(size_t)cell[i]]++] = i;
+    }
+    // the KMAX nearest points of every point, nearest first (ties by index)
+    std::vector<int> nn((size_t)m * KMAX);
+    parallel_rows(0, m, [&](int64_t a, int64_t b) {
+        std::vector<std::pair<double, int>> cand;
+        for (int64_t i = a; i < b; ++i) {
+            const int cx = cell_of((int)i, 0), cy = cell_of((int)i, 1), cz = cell_of((int)i, 2);
+            for (int r = 1;; ++r) {
+                cand.clear();
+                for (int z = std::max(0, cz - r); z <= std::min(G - 1, cz + r); ++z)
+                    for (int y = std::max(0, cy - r); y <= std::min(G - 1, cy + r); ++y)
+                        for (int x = std::max(0, cx - r); x <= std::min(G - 1, cx + r); ++x) {
+                            const int c = (z * G + y) * G + x;
+                            for (int q = cstart[c]; q < cstart[(size_t)c + 1]; ++q) {
+                                const int j = cpts[q];
+                                if (j == i) continue;
+                                double d2 = 0;
+                                for (int d = 0; d < 3; ++d) {
+                                    const double t = P[(size_t)i * 3 + d] - P[(size_t)j * 3 + d];
+                                    d2 += t * t;
+                                }
+                                cand.push_back({d2, j});
+                            }
+                        }
+                // complete once KMAX candidates lie within the searched radius r / G
+                // (every closer point is inside the searched cube) or the cube is the grid
+                const double reach = (double)r / G;
+                int inside = 0;
+                for (auto &c : cand) inside += c.first <= reach * reach;
+                if (inside >= KMAX || r >= G) break;
+            }
+            const size_t k = std::min<size_t>(KMAX, cand.size());
+            std::partial_sort(cand.begin(), cand.begin() + k, cand.end());
+            for (size_t q = 0; q < (size_t)KMAX; ++q) nn[(size_t)i * KMAX + q] = q < k ? cand[q].second : -1;
+        }
+    });
+    // per-point base k in [3, 48], log-graded across the cube (a refined
+    // region's points all have many neighbours); symmetrised degree for a scale s
+    std::vector<double> kb((size_t)m);
+    for (int i = 0; i < m; ++i) {  // spatially graded (neighbours have similar k) plus noise
+        const double g = (P[(size_t)i * 3] + P[(size_t)i * 3 + 1] + P[(size_t)i * 3 + 2]) / 3.0;
+        const double u = std::min(1.0, std::max(0.0, 1.6 * (g - 0.5) + 0.5 + 0.3 * (u01(hash3(seed, 0xF0u, (uint64_t)i)) - 0.5)));
+        kb[i] = 3.0 * std::pow(16.0, u);
+    }
+    std::vector<std::vector<int>> adj;
+    auto build = [&](double s) {
+        adj.assign((size_t)m, {});
+        for (int i = 0; i < m; ++i) {
+            const int k = std::max(1, std::min(KMAX, (int)std::lround(kb[i] * s)));
+            for (int q = 0; q < k; ++q) {
+                const int j = nn[(size_t)i * KMAX + q];
+                if (j < 0) break;
+                adj[i].push_back(j);
+                adj[j].push_back(i);
+            }
+        }
+        int64_t t = 0;
+        for (int i = 0; i < m; ++i) {
+            adj[i].push_back(i);
+            std::sort(adj[i].begin(), adj[i].end());
+            adj[i].erase(std::unique(adj[i].begin(), adj[i].end()), adj[i].end());
+            t += (int64_t)adj[i].size();
+        }
+        return t;
+    };
+    double lo = 0.05, hi = 2.0;
+    for (int it = 0; it < 40 && hi - lo > 1e-6; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        if (build(mid) < target_nnz) lo = mid;
+        else hi = mid;
+    }
+    // of the two bracketing scales, the one closer to the target
+    const int64_t tl = build(lo), th = build(hi);
+    const int64_t nnz = std::llabs(tl - target_nnz) <= std::llabs(th - target_nnz) ? build(lo) : th;
+    SMFV_REQUIRE(nnz <= 0x7fffffff, "knn3d nnz exceeds int32");
+    int *rp = xmalloc<int>((size_t)m + 1);
+    int *ci = xmalloc<int>((size_t)nnz);
+    double *va = xmalloc<double>((size_t)nnz);
+    if (!rp || !ci || !va) {
+        std::free(rp);
+        std::free(ci);
+        std::free(va);
+        set_error("out of memory");
+        return SMFV_ERR_HOST;
+    }
+    rp[0] = 0;
+    for (int i = 0; i < m; ++i) rp[i + 1] = rp[i] + (int)adj[i].size();
+    parallel_rows(0, m, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) {
+            int o = rp[i];
+            for (int j : adj[i]) {
+                ci[o] = j;
+                if (j == i) {
+                    va[o] = 1.0 + u01(hash3(seed, (uint64_t)i, (uint64_t)i));
+                } else {
+                    const uint64_t x = (uint64_t)std::min<int64_t>(i, j), y = (uint64_t)std::max<int64_t>(i, j);
+                    va[o] = 2.0 * u01(splitmix64(hash3(seed, x, y) ^ 0xA5A5A5A5ull)) - 1.0;
+                }
+                ++o;
+            }
+        }
+    });
+    *out_nnz = nnz;
+    *out_rp = rp;
+    *out_ci = ci;
+    *out_va = va;
+    return SMFV_OK;
+}
+
 SMFV_API int smfv_gen_fem27(int m, int nx, int ny, double keep, uint64_t seed, int64_t *out_nnz,
                             int **out_rp, int **out_ci, double **out_va)
 {

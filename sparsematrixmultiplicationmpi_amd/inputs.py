@@ -177,6 +177,20 @@ def cop20k_surrogate(seed: int = 20) -> SparseMatrix:
     return gen_fem27(COP20K_M, 50, 50, COP20K_KEEP, seed)
 
 
+def gen_knn3d(m: int, target_nnz: int, seed: int = 7) -> SparseMatrix:
+    """Irregular FEM-like matrix: symmetrised variable-k nearest-neighbour
+    graph of clustered 3-D points, Morton-numbered (see smfv_host.h)."""
+    return _csr_out("smfv_gen_knn3d", m, int(target_nnz), seed, m=m, n=m)
+
+
+def cop20k_irregular_surrogate(seed: int = 7) -> SparseMatrix:
+    """A second labelled stand-in for cop20k_A with its m and nnz but an
+    unstructured pattern: row degrees spread ~5..80 (cop20k_A is an FEM
+    matrix with variable row lengths; the 27-point stencil of
+    cop20k_surrogate() is regular)."""
+    return gen_knn3d(COP20K_M, COP20K_NNZ, seed)
+
+
 def permute_symmetric(A: SparseMatrix, perm: np.ndarray) -> SparseMatrix:
     """P A P^T for a square A: new row i is old row perm[i], old column c
     becomes inv[c] (inv = perm^-1), each row sorted by column.  The same

@@ -150,6 +150,49 @@ def test_cop20k_surrogate_full_size(gpu):
         assert smfv.areMatricesEqual(run(smfv.Variant.NONZERO, A, X, gpu), Yref, 1e-6)
 
 
+def test_cop20k_irregular_surrogate_full_size(gpu):
+    """The second, unstructured cop20k_A stand-in (same m and nnz; k-NN graph
+    of clustered 3-D points, row degrees 4..85) at full size: the default
+    plan tiles it and every variant's one-device result is bit-identical to
+    the reference order at K = 32 (NONZERO on the merge path within 1e-12)."""
+    A = smfv.inputs.cop20k_irregular_surrogate()
+    d = np.diff(A.rowPtr)
+    assert A.numRows == smfv.COP20K_M and abs(A.nnz - smfv.COP20K_NNZ) < 100 and d.min() <= 5 and d.max() >= 70
+    K = 32
+    X = smfv.generateLargeFatVector(A.numCols, K)
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    dA = smfv.DeviceCSR(A, gpu)
+    dX = torch.from_numpy(X).to(gpu)
+    for v in smfv.Variant:
+        plan = smfv.SpmmPlan(v, dA, K)
+        assert plan.stats()["tiled"], v
+        Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+        plan.run(dX, Y)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref)), v
+    absY = oracle.spmm("sequential", A.rowPtr, A.colIndices, np.abs(A.values), np.abs(X))
+    Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+    smfv.SpmmPlan(smfv.Variant.NONZERO, dA, K, tiles="off").run(dX, Y)
+    torch.cuda.synchronize()
+    assert rel_err(Y.cpu().numpy(), Yref, absY) <= NNZ_TOL
+
+
+def test_cop20k_surrogate_full_size_k1(gpu):
+    """Config 1's GPU line (K = 1, k_spmv_stream) at full size on the cop20k
+    surrogate: bit-identical to the reference order for every variant but
+    NONZERO (merge path, within 1e-12 x sum|a||x|)."""
+    A = smfv.cop20k_surrogate()
+    X = smfv.generateLargeFatVector(A.numCols, 1)
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    absY = oracle.spmm("sequential", A.rowPtr, A.colIndices, np.abs(A.values), np.abs(X))
+    for v in smfv.Variant:
+        Y = run(v, A, X, gpu)
+        if v == smfv.Variant.NONZERO:
+            assert rel_err(Y, Yref, absY) <= NNZ_TOL
+        else:
+            assert np.array_equal(bits(Y), bits(Yref)), v
+
+
 def test_nonzero_one_device_plan_choice(gpu):
     """NONZERO on one device: on a pattern with X-row re-use the plan takes
     the tiled row kernel and equals the sequential sum bit for bit -- what the

@@ -412,3 +412,32 @@ def test_are_matrices_equal_nan_policy():
     the C++ drop-in keeps -- documented in inputs.areMatricesEqual."""
     assert not smfv.areMatricesEqual([[1.0, float("nan")]], [[1.0, 2.0]], 1e-6)
     assert smfv.areMatricesEqual([[1.0, 2.0]], [[1.0, 2.0 + 5e-7]], 1e-6)
+
+
+def test_knn3d_irregular_surrogate():
+    """The second cop20k_A stand-in: same m, nnz within a few of 2,624,331,
+    exactly symmetric (pattern and values), diagonal present, rows sorted,
+    degrees spread 4..85 (the stencil surrogate's are 8..27), deterministic;
+    the tile analysis still tiles it (re-use >= 3)."""
+    import ctypes
+    import sparsematrixmultiplicationmpi_amd as smfv
+    from sparsematrixmultiplicationmpi_amd._lib import call
+    A = smfv.inputs.cop20k_irregular_surrogate()
+    A.validate()
+    assert A.numRows == smfv.COP20K_M and abs(A.nnz - smfv.COP20K_NNZ) <= 10
+    rp, ci, va = np.asarray(A.rowPtr), np.asarray(A.colIndices), np.asarray(A.values)
+    d = np.diff(rp)
+    assert d.min() <= 5 and d.max() >= 70 and np.percentile(d, 99) > 2 * np.median(d)
+    rows = np.repeat(np.arange(A.numRows), d)
+    assert np.all(np.diff(ci)[np.diff(rows) == 0] > 0)  # sorted, no duplicates
+    assert np.sum(rows == ci) == A.numRows  # diagonal
+    import scipy.sparse as sp
+    M = sp.csr_matrix((va, ci, rp), shape=(A.numRows, A.numCols))
+    assert abs(M - M.T).max() == 0.0
+    B = smfv.inputs.cop20k_irregular_surrogate()
+    assert np.array_equal(B.colIndices, A.colIndices) and np.array_equal(B.values, A.values)
+    out = (ctypes.c_double * 9)()
+    ip = ctypes.POINTER(ctypes.c_int)
+    rp32, ci32 = np.ascontiguousarray(rp, np.int32), np.ascontiguousarray(ci, np.int32)
+    call("smfv_plan_analyse_rows", 0, A.numRows, A.numCols, rp32.ctypes.data_as(ip), ci32.ctypes.data_as(ip), 0, out)
+    assert out[2] >= 3.0 and out[3] == 0  # re-use, direct rows
