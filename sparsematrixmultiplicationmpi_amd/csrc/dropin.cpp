@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <mpi.h>
 
+#include <sys/mman.h>
 #include <sys/resource.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -122,38 +123,51 @@ smfv_comm_t comm_world()
     return c.comm;
 }
 
-// Buffers reused across calls (grow-only): device copies of A, X, Y, the
-// kept reference result, and pinned host staging for X (in) and Y (out), so
-// a call pays no hipMalloc and its X / Y transfers run at pinned-copy speed
-// (the FatVector <-> flat conversion and the rank-0
-// rebuild are a large share of the reference's RowWise time).
+// Buffers reused across calls (grow-only): device copies of A, X, Y and the
+// kept reference result, and host staging for X (in) and Y (out), so a call
+// pays no allocation after the first.  Host staging is plain memory (on the
+// MI355X box pageable H2D / D2H run at ~50 GB/s, pinned at ~55:
+// scripts/h2d_probe.py), mapped once and faulted in 2 MiB pages (transparent
+// huge pages where the kernel allows them) -- a fresh 31 MB buffer faulted
+// 4 KiB at a time costs ~20 ms, more than the copy.
 struct Cached {
     void *p = nullptr;
     size_t cap = 0;
-    bool pinned = false;
+    bool host = false;
     void *get(size_t bytes)
     {
         if (bytes <= cap) return p;
         release();
         const size_t b = std::max<size_t>(bytes, 256);
-        if (pinned)
-            hip_check(hipHostMalloc(&p, b, hipHostMallocDefault), "hipHostMalloc");
-        else
+        if (host) {
+            const size_t huge = (size_t)2 << 20, len = (b + huge - 1) / huge * huge;
+            void *q = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            if (q == MAP_FAILED) fail("mmap of host staging failed");
+            (void)madvise(q, len, MADV_HUGEPAGE);
+            par_touch(q, len);
+            p = q;
+            cap = len;
+        } else {
             hip_check(hipMalloc(&p, b), "hipMalloc");
-        cap = b;
+            cap = b;
+        }
         return p;
     }
     void release()
     {
-        if (p) (void)(pinned ? hipHostFree(p) : hipFree(p));
+        if (p) {
+            if (host) munmap(p, cap);
+            else (void)hipFree(p);
+        }
         p = nullptr;
         cap = 0;
     }
+    // fault the pages in now, in parallel (first touch)
+    static void par_touch(void *q, size_t len);
 };
 
 struct Buffers {
     Cached rp, ci, va, X, Y, ref, hX{nullptr, 0, true}, hY{nullptr, 0, true};
-    Cached hrp{nullptr, 0, true}, hci{nullptr, 0, true}, hva{nullptr, 0, true};  // pinned A staging
     // the result of the last call on this rank (device) and the kept reference
     const double *lastY = nullptr;
     int last_m = -1, last_K = -1, ref_m = -1, ref_K = -1;
@@ -177,6 +191,15 @@ template <class F> void par_rows(int64_t rows, F f)
     std::vector<std::thread> th;
     for (int t = 0; t < nt; ++t) th.emplace_back(f, rows * t / nt, rows * (t + 1) / nt);
     for (auto &x : th) x.join();
+}
+
+void Cached::par_touch(void *q, size_t len)
+{
+    char *c = static_cast<char *>(q);
+    par_rows((int64_t)(len >> 21), [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) c[(size_t)i << 21] = 0;
+    });
+    for (size_t o = (len >> 21) << 21; o < len; o += 4096) c[o] = 0;
 }
 
 // 64-bit hash of a byte range (8-byte words, multiply-xorshift; chunks in parallel)
@@ -332,21 +355,24 @@ struct Resident {
     int64_t nnz = 0;
     uint64_t hrp = 0, hci = 0;
     uint64_t values_version = 0;  // bumped when the device values change
-    std::vector<int> rp, ci;
-    std::vector<double> va, X;  // snapshots (X row-major flat)
+    // snapshots (X row-major flat); the pattern is shared with the plan
+    // entries built from it (no second copy)
+    std::shared_ptr<std::vector<int>> rp = std::make_shared<std::vector<int>>(),
+                                      ci = std::make_shared<std::vector<int>>();
+    std::vector<double> va, X;
     Cached drp, dci, dva, dX;
     bool matches(const SparseMatrix &Am, const FatVector &f, int K_) const
     {
         return on && &Am == A && &f == fat && K_ == K && Am.numRows == m && Am.numCols == n &&
                (int64_t)Am.values.size() == nnz && (int64_t)Am.colIndices.size() == nnz &&
-               Am.rowPtr.size() == rp.size() && (int)f.size() == n;
+               Am.rowPtr.size() == rp->size() && (int)f.size() == n;
     }
-    // compare with the caller's current host objects (host preparation),
-    // then re-upload what changed (the H2D stage, opened by T.mark(0))
-    void refresh(const SparseMatrix &Am, const FatVector &f, hipStream_t st, StageTimer &T)
+    // compare with the caller's current host objects (host preparation);
+    // whatever changed is queued for upload (the H2D stage)
+    template <class Ups> void refresh(const SparseMatrix &Am, const FatVector &f, Ups &ups)
     {
-        const bool rp_new = !par_equal(Am.rowPtr.data(), rp.data(), rp.size() * sizeof(int));
-        const bool ci_new = !par_equal(Am.colIndices.data(), ci.data(), ci.size() * sizeof(int));
+        const bool rp_new = !par_equal(Am.rowPtr.data(), rp->data(), rp->size() * sizeof(int));
+        const bool ci_new = !par_equal(Am.colIndices.data(), ci->data(), ci->size() * sizeof(int));
         const bool va_new = !par_equal(Am.values.data(), va.data(), va.size() * sizeof(double));
         std::atomic<bool> xsame{true};
         par_rows(n, [&](int64_t a, int64_t b) {
@@ -354,11 +380,12 @@ struct Resident {
                 if ((int)f[i].size() != K || std::memcmp(f[i].data(), X.data() + (size_t)i * K, (size_t)K * 8))
                     xsame = false;
         });
-        if (rp_new) rp = Am.rowPtr;
-        if (ci_new) ci = Am.colIndices;
+        // (new snapshot objects: plan entries keep the old pattern they were built for)
+        if (rp_new) rp = std::make_shared<std::vector<int>>(Am.rowPtr);
+        if (ci_new) ci = std::make_shared<std::vector<int>>(Am.colIndices);
         if (rp_new || ci_new) {
-            hrp = hash_bytes(rp.data(), rp.size() * sizeof(int));
-            hci = hash_bytes(ci.data(), ci.size() * sizeof(int));
+            hrp = hash_bytes(rp->data(), rp->size() * sizeof(int));
+            hci = hash_bytes(ci->data(), ci->size() * sizeof(int));
         }
         if (va_new) {
             va = Am.values;
@@ -371,14 +398,10 @@ struct Resident {
                 for (int64_t i = a; i < b; ++i) std::copy(f[i].begin(), f[i].end(), X.data() + (size_t)i * K);
             });
         }
-        T.mark(0, st);
-        auto up = [&](void *d, const void *h, size_t bytes) {
-            if (bytes) hip_check(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
-        };
-        if (rp_new) up(drp.p, rp.data(), rp.size() * sizeof(int));
-        if (ci_new) up(dci.p, ci.data(), ci.size() * sizeof(int));
-        if (va_new) up(dva.p, va.data(), va.size() * sizeof(double));
-        if (!xsame) up(dX.p, X.data(), X.size() * sizeof(double));
+        if (rp_new) ups.push_back({drp.p, rp->data(), rp->size() * sizeof(int)});
+        if (ci_new) ups.push_back({dci.p, ci->data(), ci->size() * sizeof(int)});
+        if (va_new) ups.push_back({dva.p, va.data(), va.size() * sizeof(double)});
+        if (!xsame) ups.push_back({dX.p, X.data(), X.size() * sizeof(double)});
     }
 };
 
@@ -390,7 +413,10 @@ Resident &resident()
 
 uint64_t g_upload_version = 0;  // values uploaded by a non-resident call (always new)
 
-// A and X on the device for one call
+// A and X on the device for one call: the constructor does the host
+// preparation (checks, serialize, hashes, resident-input verification); the
+// uploads are enqueued by upload(), after the plan lookup, so the H2D stage's
+// events time only the transfers.
 struct Problem {
     int m, n, K;
     int64_t nnz;
@@ -399,7 +425,15 @@ struct Problem {
     uint64_t hrp = 0, hci = 0;  // pattern hashes (plan cache key)
     uint64_t values_id = 0;     // identifies the device values' content (skip an unchanged re-bind)
     const int *h_rp, *h_ci;     // the host pattern (verified against a cached plan's copy)
-    Problem(const SparseMatrix &A, const FatVector &fat, int K_, hipStream_t st, StageTimer &T)
+    std::shared_ptr<std::vector<int>> srp, sci;  // resident inputs: the shared pattern snapshot
+    // pending uploads (device, host, bytes)
+    struct Up {
+        void *d;
+        const void *h;
+        size_t bytes;
+    };
+    std::vector<Up> ups;
+    Problem(const SparseMatrix &A, const FatVector &fat, int K_)
         : m(A.numRows), n(A.numCols), K(K_), nnz((int64_t)A.values.size())
     {
         if ((int)A.rowPtr.size() != m + 1 || (int64_t)A.colIndices.size() != nnz ||
@@ -409,18 +443,20 @@ struct Problem {
             fail("fatVector has " + std::to_string(fat.size()) + " rows, matrix has " + std::to_string(n) + " columns");
         Buffers &B = bufs();
         Y = static_cast<double *>(B.Y.get((size_t)m * K * sizeof(double)));
-        (void)B.hY.get((size_t)m * K * sizeof(double));  // pinned Y staging (allocated here, in preparation)
+        (void)B.hY.get((size_t)m * K * sizeof(double));  // Y staging (allocated here, in preparation)
         Resident &R = resident();
         if (R.matches(A, fat, K)) {  // device-resident inputs: upload only what the caller changed
-            R.refresh(A, fat, st, T);
+            R.refresh(A, fat, ups);
             rp = static_cast<int *>(R.drp.p);
             ci = static_cast<int *>(R.dci.p);
             va = static_cast<double *>(R.dva.p);
             X = static_cast<double *>(R.dX.p);
             hrp = R.hrp;
             hci = R.hci;
-            h_rp = R.rp.data();
-            h_ci = R.ci.data();
+            srp = R.rp;
+            sci = R.ci;
+            h_rp = srp->data();
+            h_ci = sci->data();
             values_id = (R.values_version << 1) | 1;
             return;
         }
@@ -430,37 +466,28 @@ struct Problem {
         ci = static_cast<int *>(B.ci.get(A.colIndices.size() * sizeof(int)));
         va = static_cast<double *>(B.va.get(A.values.size() * sizeof(double)));
         X = static_cast<double *>(B.X.get((size_t)n * K * sizeof(double)));
-        // serialize (SC/utils.cpp:216-228) straight into pinned staging, and
-        // A's arrays too: the DMA then runs at pinned-copy speed (a pageable
-        // source is copied through a driver bounce buffer at a fraction of it)
+        // serialize (SC/utils.cpp:216-228) into the staging buffer
         double *hx = static_cast<double *>(B.hX.get((size_t)n * K * sizeof(double)));
         par_rows(n, [&](int64_t a, int64_t b) {
             for (int64_t i = a; i < b; ++i) std::copy(fat[i].begin(), fat[i].end(), hx + (size_t)i * K);
         });
-        auto stage = [&](Cached &c, const void *src, size_t bytes) -> const void * {
-            void *h = c.get(bytes);
-            par_rows((int64_t)(bytes >> 16) + 1, [&](int64_t lo, int64_t hi) {
-                const size_t s0 = (size_t)lo << 16, e0 = std::min(bytes, (size_t)hi << 16);
-                if (s0 < e0) std::memcpy(static_cast<char *>(h) + s0, static_cast<const char *>(src) + s0, e0 - s0);
-            });
-            return h;
-        };
-        const void *hrp_ = stage(B.hrp, A.rowPtr.data(), A.rowPtr.size() * sizeof(int));
-        const void *hci_ = stage(B.hci, A.colIndices.data(), A.colIndices.size() * sizeof(int));
-        const void *hva_ = stage(B.hva, A.values.data(), A.values.size() * sizeof(double));
         hrp = hash_bytes(A.rowPtr.data(), A.rowPtr.size() * sizeof(int));
         hci = hash_bytes(A.colIndices.data(), A.colIndices.size() * sizeof(int));
         h_rp = A.rowPtr.data();
         h_ci = A.colIndices.data();
         values_id = (++g_upload_version) << 1;
+        ups.push_back({rp, A.rowPtr.data(), A.rowPtr.size() * sizeof(int)});
+        ups.push_back({ci, A.colIndices.data(), A.colIndices.size() * sizeof(int)});
+        ups.push_back({va, A.values.data(), A.values.size() * sizeof(double)});
+        ups.push_back({X, hx, (size_t)n * K * sizeof(double)});
+    }
+    // the H2D stage: T.mark(0), the uploads
+    void upload(hipStream_t st, StageTimer &T)
+    {
         T.mark(0, st);
-        auto up = [&](void *d, const void *h, size_t bytes) {
-            if (bytes) hip_check(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
-        };
-        up(rp, hrp_, A.rowPtr.size() * sizeof(int));
-        up(ci, hci_, A.colIndices.size() * sizeof(int));
-        up(va, hva_, A.values.size() * sizeof(double));
-        up(X, hx, (size_t)n * K * sizeof(double));
+        for (const Up &u : ups)
+            if (u.bytes) hip_check(hipMemcpyAsync(u.d, u.h, u.bytes, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+        ups.clear();
     }
     FatVector download(hipStream_t st, StageTimer &T)
     {
@@ -538,7 +565,7 @@ struct Plans {  // one plan of a variant: single-device or distributed
 
 struct PlanEntry {
     PlanKey key;
-    std::vector<int> rp, ci;        // the pattern this entry's plans were built for
+    std::shared_ptr<const std::vector<int>> rp, ci;  // the pattern this entry's plans were built for
     Plans untiled;                  // created with the entry (SMFV_PLAN_NO_TILES)
     Plans tiled;                    // the background build's result, once taken
     std::future<Plans> building;    // the background build (valid until taken)
@@ -610,8 +637,8 @@ PlanEntry &plan_for(int variant, const Problem &P, int world)
     auto &v = plans();
     PlanEntry *e = nullptr;
     for (auto &x : v)
-        if (x->key == key && par_equal(x->rp.data(), P.h_rp, x->rp.size() * sizeof(int)) &&
-            par_equal(x->ci.data(), P.h_ci, x->ci.size() * sizeof(int))) {
+        if (x->key == key && (x->rp->data() == P.h_rp || par_equal(x->rp->data(), P.h_rp, x->rp->size() * sizeof(int))) &&
+            (x->ci->data() == P.h_ci || par_equal(x->ci->data(), P.h_ci, x->ci->size() * sizeof(int)))) {
             e = x.get();
             break;
         }
@@ -623,12 +650,15 @@ PlanEntry &plan_for(int variant, const Problem &P, int world)
         }
         auto ne = std::make_unique<PlanEntry>();
         ne->key = key;
-        ne->rp.assign(P.h_rp, P.h_rp + P.m + 1);
-        ne->ci.assign(P.h_ci, P.h_ci + P.nnz);
+        // the entry's own pattern: the resident snapshot shared, else a copy
+        ne->rp = P.srp ? std::shared_ptr<const std::vector<int>>(P.srp)
+                       : std::make_shared<const std::vector<int>>(P.h_rp, P.h_rp + P.m + 1);
+        ne->ci = P.sci ? std::shared_ptr<const std::vector<int>>(P.sci)
+                       : std::make_shared<const std::vector<int>>(P.h_ci, P.h_ci + P.nnz);
         if (world > 1) (void)comm_world();  // the communicator exists before any thread needs it
         int dev = 0;
         hip_check(hipGetDevice(&dev), "hipGetDevice");
-        ne->untiled = create_plans(variant, P.m, P.n, P.nnz, ne->rp.data(), ne->ci.data(), P.K, world,
+        ne->untiled = create_plans(variant, P.m, P.n, P.nnz, ne->rp->data(), ne->ci->data(), P.K, world,
                                    SMFV_PLAN_NO_TILES | (variant == SMFV_SEQUENTIAL ? SMFV_PLAN_SIMPLE_ROWS : 0), dev);
         if (!ne->untiled.local && !ne->untiled.dist) check(SMFV_ERR_INVALID, "smfv plan create (untiled)");
         const bool may_tile = variant != SMFV_SEQUENTIAL && P.K % 32 == 0 && P.m > 0 && P.nnz > 0;
@@ -666,8 +696,8 @@ void start_pending_builds()
         raw->building = std::async(std::launch::async, [raw]() {
             setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), 10);  // behind the caller's own work
             smfv_set_analysis_threads(4);
-            return create_plans(raw->key.variant, raw->key.m, raw->key.n, raw->key.nnz, raw->rp.data(),
-                                raw->ci.data(), raw->key.K, raw->world, 0, raw->device);
+            return create_plans(raw->key.variant, raw->key.m, raw->key.n, raw->key.nnz, raw->rp->data(),
+                                raw->ci->data(), raw->key.K, raw->world, 0, raw->device);
         });
     }
 }
@@ -692,8 +722,9 @@ FatVector local_run(int variant, const SparseMatrix &A, const FatVector &fat, in
 {
     Context &c = ctx();
     StageTimer T;
-    Problem P(A, fat, K, c.stream, T);
+    Problem P(A, fat, K);
     PlanEntry &e = plan_for(variant, P, 1);
+    P.upload(c.stream, T);
     T.mark(1, c.stream);
     Plans &pl = bound_plan(&e, P, c.stream);
     check(smfv_plan_execute(pl.local, P.rp, P.ci, P.va, P.X, K, P.Y, K, c.stream), "smfv_plan_execute");
@@ -711,8 +742,9 @@ FatVector collective_run(int variant, const SparseMatrix &A, const FatVector &fa
     Context &c = ctx();
     if (c.size == 1) return local_run(variant, A, fat, K, name);
     StageTimer T;
-    Problem P(A, fat, K, c.stream, T);
+    Problem P(A, fat, K);
     PlanEntry &e = plan_for(variant, P, c.size);
+    P.upload(c.stream, T);
     T.mark(1, c.stream);
     Plans &pl = bound_plan(&e, P, c.stream);
     check(smfv_dist_plan_execute_local(pl.dist, P.rp, P.ci, P.va, P.X, P.Y, c.stream), "smfv_dist_plan_execute_local");
@@ -842,12 +874,12 @@ DROPIN_API double smfvDistributeInputs(SparseMatrix &A, FatVector &fat, int k)
     R.n = n;
     R.K = K;
     R.nnz = nnz;
-    R.rp = A.rowPtr;
-    R.ci = A.colIndices;
+    R.rp = std::make_shared<std::vector<int>>(A.rowPtr);
+    R.ci = std::make_shared<std::vector<int>>(A.colIndices);
     R.va = A.values;
     R.X.assign(hx, hx + (size_t)n * K);
-    R.hrp = hash_bytes(R.rp.data(), R.rp.size() * sizeof(int));
-    R.hci = hash_bytes(R.ci.data(), R.ci.size() * sizeof(int));
+    R.hrp = hash_bytes(R.rp->data(), R.rp->size() * sizeof(int));
+    R.hci = hash_bytes(R.ci->data(), R.ci->size() * sizeof(int));
     ++R.values_version;
     R.on = true;
     return MPI_Wtime() - t0;
@@ -857,8 +889,8 @@ DROPIN_API void smfvReleaseInputs()
 {
     Resident &R = resident();
     R.on = false;
-    R.rp = {};
-    R.ci = {};
+    R.rp = std::make_shared<std::vector<int>>();
+    R.ci = std::make_shared<std::vector<int>>();
     R.va = {};
     R.X = {};
 }

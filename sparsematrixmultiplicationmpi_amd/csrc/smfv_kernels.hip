@@ -259,6 +259,99 @@ __global__ __launch_bounds__(NT) void k_spmv_stream(int row_begin, int nrows, co
 }
 
 // ---------------------------------------------------------------------------
+// k_spmv_pipe: K = 1 with the row groups of k_spmv_stream (RPB rows, their
+// non-zeros in CH-entry chunks) dealt to fewer blocks, each of which runs its
+// chunks as a two-stage software pipeline: the (col, val) loads of the NEXT
+// chunk -- of this group, or the first of the block's next group, whose
+// row_ptr slice was loaded one group ahead -- are issued before this chunk's
+// X gathers, products and per-row sums, so the CSR stream keeps flowing
+// while a chunk's dependent steps run.  Same products, same per-row CSR-order
+// sums as k_spmv_stream: bit-identical.
+// ---------------------------------------------------------------------------
+template <int NT, int RPB, int CH>
+__global__ __launch_bounds__(NT) void k_spmv_pipe(int row_begin, int nrows, int ngroups,
+                                                  const int *__restrict__ rp, const int *__restrict__ ci,
+                                                  const double *__restrict__ va, const double *__restrict__ X,
+                                                  int64_t ldx, double *__restrict__ Y, int64_t ldy)
+{
+    static_assert(CH % NT == 0 && RPB <= NT, "whole products per lane, one lane per row");
+    constexpr int PER = CH / NT;
+    __shared__ double prod[CH];
+    const int nb = gridDim.x, t = threadIdx.x;
+    int g = xcd_remap(blockIdx.x, nb);
+    if (g >= ngroups) return;  // block-uniform
+    // a group's extent: rows [r0, r0 + nr), non-zeros [e0, e1), this lane's row [js, je)
+    struct Grp {
+        int nr;
+        int64_t e0, e1;
+        int js, je;
+    };
+    auto group = [&](int gg) {
+        Grp q{0, 0, 0, 0, 0};
+        if (gg >= ngroups) return q;
+        const int lr0 = gg * RPB;
+        q.nr = min(RPB, nrows - lr0);
+        const int r0 = row_begin + lr0;
+        q.e0 = rp[r0];
+        q.e1 = rp[r0 + q.nr];
+        if (t < q.nr) q.js = rp[r0 + t], q.je = rp[r0 + t + 1];
+        return q;
+    };
+    auto load = [&](int64_t c0, int64_t e1, int (&c)[PER], double (&v)[PER]) {
+        const int cn = (int)min((int64_t)CH, e1 - c0);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int e = t + i * NT;
+            c[i] = e < cn ? __builtin_nontemporal_load(ci + c0 + e) : 0;
+            v[i] = e < cn ? __builtin_nontemporal_load(va + c0 + e) : 0.0;
+        }
+    };
+    Grp cur = group(g), nxt = group(g + nb);
+    int64_t c0 = cur.e0;  // current chunk start
+    int c[PER], nc[PER];
+    double v[PER], nv[PER];
+    load(c0, cur.e1, c, v);
+    double acc = 0.0;
+    for (;;) {
+        // the next chunk: the rest of this group, else the block's next group
+        const bool same = c0 + CH < cur.e1;
+        const int64_t n0 = same ? c0 + CH : nxt.e0;
+        const bool more = same || g + nb < ngroups;
+        if (more) load(n0, same ? cur.e1 : nxt.e1, nc, nv);
+        // this chunk: X gathers, products to LDS, per-row sums in CSR order
+        const int cn = (int)min((int64_t)CH, cur.e1 - c0);
+        double x[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) x[i] = t + i * NT < cn ? X[(int64_t)c[i] * ldx] : 0.0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) prod[t + i * NT] = v[i] * x[i];
+        __syncthreads();
+        int j = (int)(max((int64_t)cur.js, c0) - c0);
+        const int b = (int)(min((int64_t)cur.je, c0 + cn) - c0);
+        for (; j + 4 <= b; j += 4) {
+            const double p0 = prod[j], p1 = prod[j + 1], p2 = prod[j + 2], p3 = prod[j + 3];
+            acc = acc + p0;
+            acc = acc + p1;
+            acc = acc + p2;
+            acc = acc + p3;
+        }
+        for (; j < b; ++j) acc = acc + prod[j];
+        __syncthreads();
+        if (!same) {  // the group is complete
+            if (t < cur.nr) Y[(int64_t)(g * RPB + t) * ldy] = acc;
+            acc = 0.0;
+            if (!more) break;
+            g += nb;
+            cur = nxt;
+            nxt = group(g + nb);  // one group ahead
+        }
+        c0 = n0;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) c[i] = nc[i], v[i] = nv[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_rows_mh: the production row kernel for K even and 16-byte aligned X/Y.
 //
 //  * a block of 256 lanes owns 256/TEAM consecutive rows; it stages its
@@ -1271,6 +1364,19 @@ static int launch_rows(int row_begin, int nrows, const int *rp, const int *ci, c
         constexpr int NT = 256, RPB = 64, CH = 2048;
         const int64_t nblk = ((int64_t)nrows + RPB - 1) / RPB;
         SMFV_REQUIRE(nblk <= 0x7fffffff, "too many rows for one launch");
+#ifdef SMFV_LAB
+        static const int pipe_bpc = [] {  // lab A/B: SMFV_K1_PIPE=<blocks per CU> runs k_spmv_pipe
+            const char *e = std::getenv("SMFV_K1_PIPE");
+            return e ? std::atoi(e) : 0;
+        }();
+        if (pipe_bpc > 0) {
+            const int64_t pb = std::min<int64_t>(nblk, (int64_t)256 * pipe_bpc);
+            hipLaunchKernelGGL((k_spmv_pipe<NT, RPB, CH>), dim3((unsigned)pb), dim3(NT), 0, st, row_begin, nrows,
+                               (int)nblk, rp, ci, va, X, ldx, Y, ldy);
+            SMFV_LAUNCHED();
+            return SMFV_OK;
+        }
+#endif
         hipLaunchKernelGGL((k_spmv_stream<NT, RPB, CH>), dim3((unsigned)nblk), dim3(NT), 0, st, row_begin, nrows,
                            rp, ci, va, X, ldx, Y, ldy);
         SMFV_LAUNCHED();
