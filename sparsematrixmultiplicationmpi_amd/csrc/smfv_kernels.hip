@@ -258,98 +258,9 @@ __global__ __launch_bounds__(NT) void k_spmv_stream(int row_begin, int nrows, co
     if (t < nr) Y[(int64_t)(lr0 + t) * ldy] = acc;
 }
 
-// ---------------------------------------------------------------------------
-// k_spmv_pipe: K = 1 with the row groups of k_spmv_stream (RPB rows, their
-// non-zeros in CH-entry chunks) dealt to fewer blocks, each of which runs its
-// chunks as a two-stage software pipeline: the (col, val) loads of the NEXT
-// chunk -- of this group, or the first of the block's next group, whose
-// row_ptr slice was loaded one group ahead -- are issued before this chunk's
-// X gathers, products and per-row sums, so the CSR stream keeps flowing
-// while a chunk's dependent steps run.  Same products, same per-row CSR-order
-// sums as k_spmv_stream: bit-identical.
-// ---------------------------------------------------------------------------
-template <int NT, int RPB, int CH>
-__global__ __launch_bounds__(NT) void k_spmv_pipe(int row_begin, int nrows, int ngroups,
-                                                  const int *__restrict__ rp, const int *__restrict__ ci,
-                                                  const double *__restrict__ va, const double *__restrict__ X,
-                                                  int64_t ldx, double *__restrict__ Y, int64_t ldy)
-{
-    static_assert(CH % NT == 0 && RPB <= NT, "whole products per lane, one lane per row");
-    constexpr int PER = CH / NT;
-    __shared__ double prod[CH];
-    const int nb = gridDim.x, t = threadIdx.x;
-    int g = xcd_remap(blockIdx.x, nb);
-    if (g >= ngroups) return;  // block-uniform
-    // a group's extent: rows [r0, r0 + nr), non-zeros [e0, e1), this lane's row [js, je)
-    struct Grp {
-        int nr;
-        int64_t e0, e1;
-        int js, je;
-    };
-    auto group = [&](int gg) {
-        Grp q{0, 0, 0, 0, 0};
-        if (gg >= ngroups) return q;
-        const int lr0 = gg * RPB;
-        q.nr = min(RPB, nrows - lr0);
-        const int r0 = row_begin + lr0;
-        q.e0 = rp[r0];
-        q.e1 = rp[r0 + q.nr];
-        if (t < q.nr) q.js = rp[r0 + t], q.je = rp[r0 + t + 1];
-        return q;
-    };
-    auto load = [&](int64_t c0, int64_t e1, int (&c)[PER], double (&v)[PER]) {
-        const int cn = (int)min((int64_t)CH, e1 - c0);
-#pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int e = t + i * NT;
-            c[i] = e < cn ? __builtin_nontemporal_load(ci + c0 + e) : 0;
-            v[i] = e < cn ? __builtin_nontemporal_load(va + c0 + e) : 0.0;
-        }
-    };
-    Grp cur = group(g), nxt = group(g + nb);
-    int64_t c0 = cur.e0;  // current chunk start
-    int c[PER], nc[PER];
-    double v[PER], nv[PER];
-    load(c0, cur.e1, c, v);
-    double acc = 0.0;
-    for (;;) {
-        // the next chunk: the rest of this group, else the block's next group
-        const bool same = c0 + CH < cur.e1;
-        const int64_t n0 = same ? c0 + CH : nxt.e0;
-        const bool more = same || g + nb < ngroups;
-        if (more) load(n0, same ? cur.e1 : nxt.e1, nc, nv);
-        // this chunk: X gathers, products to LDS, per-row sums in CSR order
-        const int cn = (int)min((int64_t)CH, cur.e1 - c0);
-        double x[PER];
-#pragma unroll
-        for (int i = 0; i < PER; ++i) x[i] = t + i * NT < cn ? X[(int64_t)c[i] * ldx] : 0.0;
-#pragma unroll
-        for (int i = 0; i < PER; ++i) prod[t + i * NT] = v[i] * x[i];
-        __syncthreads();
-        int j = (int)(max((int64_t)cur.js, c0) - c0);
-        const int b = (int)(min((int64_t)cur.je, c0 + cn) - c0);
-        for (; j + 4 <= b; j += 4) {
-            const double p0 = prod[j], p1 = prod[j + 1], p2 = prod[j + 2], p3 = prod[j + 3];
-            acc = acc + p0;
-            acc = acc + p1;
-            acc = acc + p2;
-            acc = acc + p3;
-        }
-        for (; j < b; ++j) acc = acc + prod[j];
-        __syncthreads();
-        if (!same) {  // the group is complete
-            if (t < cur.nr) Y[(int64_t)(g * RPB + t) * ldy] = acc;
-            acc = 0.0;
-            if (!more) break;
-            g += nb;
-            cur = nxt;
-            nxt = group(g + nb);  // one group ahead
-        }
-        c0 = n0;
-#pragma unroll
-        for (int i = 0; i < PER; ++i) c[i] = nc[i], v[i] = nv[i];
-    }
-}
+#ifdef SMFV_LAB
+#include "lab/spmv_lab.inc"  // k_spmv_pipe (lab A/B, measured slower: DESIGN.md section 7)
+#endif
 
 // ---------------------------------------------------------------------------
 // k_rows_mh: the production row kernel for K even and 16-byte aligned X/Y.
@@ -554,40 +465,12 @@ template <bool NT> __device__ __forceinline__ void dma16s(const void *base, unsi
 __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 }  // namespace ws
 
-// ABL (lab A/B only: instantiated in the lab build, libsmfv_lab.so with
-// -DSMFV_LAB, selected there by SMFV_WS_ABL; libsmfv.so has ABL = 0 only):
-// 1 staging only (no compute), 2 compute
-// only (every unit recomputes the first staged tile), 3 as 2 without Y stores,
-// 4 as 2 without the per-unit barriers (waves run their units unsynchronised),
-// 5 staging and compute both running, decoupled (no barriers; compute reads
-// slot 0 while it is restaged: timing only, results are garbage), 6 as 2 with
-// half the X reads (the other half synthesised by a multiply; timing only),
-// 7 the full kernel without Y stores (timing only)
 // SADDR: the loaders address X, the values and the offsets by scalar base +
 // 32-bit byte offset (X and the plan's arrays each < 4 GiB; the host picks it).
 struct WsXcd {
     int first[9];  // XCD x runs tiles [first[x], first[x + 1]) of the plan's order
 };
-#ifdef SMFV_LAB
-// lab ABL 8: per (block, wave, unit) two s_memtime stamps -- compute waves:
-// unit start (after its barrier), rows stored; loader waves: the next unit's
-// DMAs issued, landed (vmcnt 0) -- written by lane 0 with vector stores
-__device__ unsigned long long *ws_stamps = nullptr;
-constexpr int WS_STAMP_UNITS = 32;
-#define WS_STAMP(ABL_, u_, k_)                                                                                    \
-    do {                                                                                                          \
-        if constexpr (ABL_ == 8)                                                                                  \
-            if (lane == 0 && (u_) < WS_STAMP_UNITS)                                                               \
-                ((__attribute__((address_space(1))) unsigned long long *)ws_stamps)                               \
-                    [(((size_t)blockIdx.x * 16 + wv) * WS_STAMP_UNITS + (u_)) * 2 + (k_)] =                       \
-                        __builtin_amdgcn_s_memtime(); /* global (vector) store: not counted by lgkmcnt */         \
-    } while (0)
-#else
-#define WS_STAMP(ABL_, u_, k_) \
-    do {                       \
-    } while (0)
-#endif
-template <int ABL, bool FMA = false, bool SADDR = true>
+template <bool FMA = false, bool SADDR = true>
 __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int chunked,
                                                      const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
@@ -700,16 +583,14 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
         int it = 0, p = 0;  // unit u + 1 to stage
         if (++p == npanel) p = 0, ++it;
         for (int u = 0; u < nunits; ++u) {
-            if (u + 1 < nunits && ABL != 2 && ABL != 3 && ABL != 4 && ABL != 6) {
+            if (u + 1 < nunits) {
                 const int t = t0 + it * tstep;
                 stage(t, p, (u + 1) & 1, it & 1);
                 if (p == npanel - 1) fetch_record(min(t + tstep, tlast));
                 if (++p == npanel) p = 0, ++it;
             }
-            WS_STAMP(ABL, u, 0);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // unit u+1 has landed
-            WS_STAMP(ABL, u, 1);
-            if (ABL != 4 && ABL != 5) barrier_lds();
+            barrier_lds();
         }
         return;
     }
@@ -728,14 +609,11 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
     barrier_lds();
     int it = 0, p = 0;
     for (int u = 0; u < nunits; ++u) {
-        // (ABL 2-6 recompute the prologue's unit: slot 0 is the only staged one)
-        constexpr bool SLOT0 = ABL >= 2 && ABL <= 6;
-        const char *xbase = lds + (SLOT0 ? 0 : (u & 1)) * XSLOT;
-        const char *mbase = lds + SL_M + (SLOT0 ? 0 : (it & 1)) * MSLOT;
-        WS_STAMP(ABL, u, 0);
+        const char *xbase = lds + (u & 1) * XSLOT;
+        const char *mbase = lds + SL_M + (it & 1) * MSLOT;
         const int *R = reinterpret_cast<const int *>(mbase + M_R);
         const int row = R[slot];
-        if (row >= 0 && ABL != 1) {
+        if (row >= 0) {
             const int info = R[64 + slot];
             // the row runs nbat whole batches of 8, then rem (0, 2, 4 or 6)
             // entries of one more (its length rounded up to even)
@@ -753,13 +631,8 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
             auto rdx = [&](unsigned w, d2 &a0, d2 &a1, d2 &b0, d2 &b1) {
                 a0 = *reinterpret_cast<const d2 *>(xb0 + (w & 0xFFFF));
                 b0 = *reinterpret_cast<const d2 *>(xb0 + (w >> 16));
-                if constexpr (ABL == 6) {  // lab: half the X reads (timing only)
-                    a1 = a0 * 1.5;
-                    b1 = b0 * 1.5;
-                } else {
-                    a1 = *reinterpret_cast<const d2 *>(xb1 + (w & 0xFFFF));
-                    b1 = *reinterpret_cast<const d2 *>(xb1 + (w >> 16));
-                }
+                a1 = *reinterpret_cast<const d2 *>(xb1 + (w & 0xFFFF));
+                b1 = *reinterpret_cast<const d2 *>(xb1 + (w >> 16));
             };
             u4 ln = Lq[0];
             d2 vn[4];
@@ -828,18 +701,17 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
             // DMAs: stores deferred into the next unit, among the loaders'
             // DMA issue, measured 25.6 -> 28.1 us)
             double *y = Y + (int64_t)row * ldy + p * TILE_KP + 2 * tl;
-            if ((ABL != 3 && ABL != 7) || acc0.x != acc0.x) {
-                __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y + 16 * par));
-                __builtin_nontemporal_store(acc1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
-            }
+            __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y + 16 * par));
+            __builtin_nontemporal_store(acc1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
         }
-        WS_STAMP(ABL, u, 1);
         if (++p == npanel) p = 0, ++it;
-        if (ABL != 4 && ABL != 5) {
-            barrier_lds();  // X slot (u & 1) is free for unit u + 2, meta slot for tile it + 1
-        }
+        barrier_lds();  // X slot (u & 1) is free for unit u + 2, meta slot for tile it + 1
     }
 }
+
+#ifdef SMFV_LAB
+#include "lab/ws_lab.inc"  // the instrumented lab copy (libsmfv_lab.so only)
+#endif
 
 // Rows the ws plan could not tile (over a cap alone): one 8-lane team per
 // row, X gathered straight from HBM, CSR order (bit-identical).  `rows` are
@@ -2070,11 +1942,11 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             return e ? std::atoi(e) : -1;
         }();
         if (lab_chunked >= 0) chunked = lab_chunked;
-        auto kern = plan->fma ? (abl == 2 ? k_rows_ws<2, true> : k_rows_ws<0, true>)
-                  : abl == 1 ? k_rows_ws<1> : abl == 2 ? k_rows_ws<2> : abl == 3 ? k_rows_ws<3>
-                  : abl == 4 ? k_rows_ws<4> : abl == 5 ? k_rows_ws<5> : abl == 6 ? k_rows_ws<6>
-                  : abl == 7 ? k_rows_ws<7> : abl == 8 ? k_rows_ws<8> : k_rows_ws<0>;
-        if (!(saddr && lab_saddr)) kern = plan->fma ? k_rows_ws<0, true, false> : k_rows_ws<0, false, false>;
+        auto kern = plan->fma ? (abl == 2 ? k_rows_ws_lab<2, true> : k_rows_ws<true>)
+                  : abl == 1 ? k_rows_ws_lab<1> : abl == 2 ? k_rows_ws_lab<2> : abl == 3 ? k_rows_ws_lab<3>
+                  : abl == 4 ? k_rows_ws_lab<4> : abl == 5 ? k_rows_ws_lab<5> : abl == 6 ? k_rows_ws_lab<6>
+                  : abl == 7 ? k_rows_ws_lab<7> : abl == 8 ? k_rows_ws_lab<8> : k_rows_ws<>;
+        if (!(saddr && lab_saddr)) kern = plan->fma ? k_rows_ws<true, false> : k_rows_ws<false, false>;
         static unsigned long long *stamp_buf = nullptr;
         const size_t stamp_n = (size_t)blocks * 16 * WS_STAMP_UNITS * 2;
         if (abl == 8 && !stamp_buf) {
@@ -2084,8 +1956,8 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         SMFV_REQUIRE(abl != 8 || blocks <= 256, "lab stamps: at most 256 blocks");
         if (abl == 8) SMFV_HIP(hipMemsetAsync(stamp_buf, 0, stamp_n * 8, st));
 #else
-        auto kern = saddr ? (plan->fma ? k_rows_ws<0, true> : k_rows_ws<0>)
-                          : (plan->fma ? k_rows_ws<0, true, false> : k_rows_ws<0, false, false>);
+        auto kern = saddr ? (plan->fma ? k_rows_ws<true> : k_rows_ws<>)
+                          : (plan->fma ? k_rows_ws<true, false> : k_rows_ws<false, false>);
 #endif
         WsXcd xr;
         for (int x = 0; x <= 8; ++x) xr.first[x] = plan->ws_xcd[x];
