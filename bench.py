@@ -732,6 +732,9 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rows", type=int, default=0, help="syn80m_k32: matrix rows (default 80M)")
     ap.add_argument("--no-vendor", action="store_true", help="skip the rocSPARSE comparator leg")
+    ap.add_argument("--no-warm", action="store_true",
+                    help="skip the same-copy (warm) leg: every launch of the process streams from HBM "
+                         "(for a cold-only rocprofv3 kernel trace)")
     ap.add_argument("--no-check", action="store_true",
                     help="report the post-timing result check but do not fail on it (lab ablations)")
     ap.add_argument("--mfma", action="store_true",
@@ -848,7 +851,9 @@ def main() -> None:
     # beside `value`, which stays the first timed region
     samples = sorted([span_ms] + [timed(g_cold) for _ in range(9)])
     del g_cold
-    span_ms_w = timed(capture(True))
+    # the warm leg (same copy every launch) after the cold one; --no-warm
+    # leaves it out so a profile of this process holds cold launches only
+    span_ms_w = timed(capture(True)) if not args.no_warm else float("nan")
     stream_gbps = stream_copy_gbps(dev)
     vendor = None
     if variant in ("ROWWISE", "SEQUENTIAL") and not args.no_vendor:
@@ -930,9 +935,10 @@ def main() -> None:
                               "GBps": round((prob_bytes + 8 * nnz * K) / (kern_ms * 1e-3) / 1e9, 1),
                               "note": "random columns: one X row gathered per non-zero (SURVEY 8d config 4)"}
                              if kind == "pow10m" else None),
-            "warm": {"note": "same copy every launch (working set in the 256 MiB Infinity Cache)",
-                     "avg_launch_ms": round(kern_ms_w, 6), "achieved_GBps": round(achieved_w, 1),
-                     "GFLOPs": round(world * flops / (span_ms_w / args.steps * 1e-3) / 1e9, 3)},
+            "warm": ({"note": "same copy every launch (working set in the 256 MiB Infinity Cache)",
+                      "avg_launch_ms": round(kern_ms_w, 6), "achieved_GBps": round(achieved_w, 1),
+                      "GFLOPs": round(world * flops / (span_ms_w / args.steps * 1e-3) / 1e9, 3)}
+                     if not args.no_warm else None),
             "effective_GFLOPs_per_gpu": round(flops / (ms_per_step * 1e-3) / 1e9, 3),
             "check": chk,
             "cpu_baseline": cpu,
