@@ -15,6 +15,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -354,6 +356,7 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
     }
     if ((int64_t)P.loff.size() != P.entries + WS_SLACK || P.tsrc.size() != P.loff.size())
         return fail("entry arrays");
+    // headers and row ownership (sequential: every row in exactly one place)
     for (int t = 0; t < P.ntiles; ++t) {
         const int *g = &P.grec[(size_t)t * WS_GWORDS];
         const int *l = &P.lrec[(size_t)t * WS_LWORDS];
@@ -364,36 +367,11 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
         if (noff % 32 || tn % 32 || tn <= 0 || tn > WS_NCAP || nu < 0 || nu > WS_UCAP ||
             (int64_t)noff + tn > P.entries)
             return fail("tile header out of range");
-        for (int q = 0; q < 256; ++q)
-            if (g[q] < 0 || g[q] >= n) return fail("union id out of range");
-        for (int e = noff; e < noff + tn; ++e)
-            if (P.loff[e] != WS_ZOFF && (P.loff[e] % 256 || P.loff[e] / 256 >= nu))
-                return fail("entry offset outside the tile's union");
         for (int slot = 0; slot < WS_ROWS; ++slot) {
             const int r = l[slot];
             if (r == -1) continue;
             if (r < 0 || r >= m || seen[r]) return fail("tile row out of range or repeated");
             seen[r] = 1;
-            const int lb = l[64 + slot] & 0xFFFF, len = l[64 + slot] >> 16, vb = l[128 + slot];
-            const int k = (slot >> 3) & 3;
-            const int rl = rp[r + 1] - rp[r];
-            if (len % 2 || len < rl || len > rl + 1) return fail("row segment length");
-            for (int b = 0; b < (len + 7) / 8; ++b)
-                for (int u = 0; u < 8; ++u) {
-                    const int el = 8 * b + u;
-                    const int64_t le = (int64_t)noff + (int64_t)(lb + 4 * b + k) * 8 + u;
-                    const int64_t ve = (int64_t)noff + (int64_t)(vb + 4 * (4 * b + u / 2) + k) * 2 + u % 2;
-                    if (le >= noff + tn || ve >= noff + tn) return fail("segment leaves its tile");
-                    if (el < rl) {
-                        const int j = rp[r] + el;
-                        const int u_ = P.loff[le] / 256;
-                        const int w = (u_ / 4) / 8, i = (u_ / 4) % 8, qq = u_ % 4;
-                        if (P.tsrc[ve] != j || P.loff[le] == WS_ZOFF || u_ >= nu || g[32 * w + 8 * qq + i] != ci[j])
-                            return fail("row entry is not its CSR non-zero");
-                    } else if (P.tsrc[ve] != -1 || P.loff[le] != WS_ZOFF) {
-                        return fail("pad entry does not read the zero row");
-                    }
-                }
         }
     }
     for (int r = 0; r < m; ++r)
@@ -401,6 +379,56 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
     if (P.xcd[0] != 0 || P.xcd[8] != P.ntiles) return fail("XCD ranges do not cover the tiles");
     for (int x = 0; x < 8; ++x)
         if (P.xcd[x] > P.xcd[x + 1]) return fail("XCD ranges out of order");
+    // every tile's entries, replayed as the kernel reads them (tiles in parallel)
+    auto check_tile = [&](int t) -> const char * {
+        const int *g = &P.grec[(size_t)t * WS_GWORDS];
+        const int *l = &P.lrec[(size_t)t * WS_LWORDS];
+        const int noff = g[WS_G_NOFF], tn = g[WS_G_TN], nu = g[WS_G_NU];
+        for (int q = 0; q < 256; ++q)
+            if (g[q] < 0 || g[q] >= n) return "union id out of range";
+        for (int e = noff; e < noff + tn; ++e)
+            if (P.loff[e] != WS_ZOFF && (P.loff[e] % 256 || P.loff[e] / 256 >= nu))
+                return "entry offset outside the tile's union";
+        for (int slot = 0; slot < WS_ROWS; ++slot) {
+            const int r = l[slot];
+            if (r == -1) continue;
+            const int lb = l[64 + slot] & 0xFFFF, len = l[64 + slot] >> 16, vb = l[128 + slot];
+            const int k = (slot >> 3) & 3;
+            const int rl = rp[r + 1] - rp[r];
+            if (len % 2 || len < rl || len > rl + 1) return "row segment length";
+            for (int b = 0; b < (len + 7) / 8; ++b)
+                for (int u = 0; u < 8; ++u) {
+                    const int el = 8 * b + u;
+                    const int64_t le = (int64_t)noff + (int64_t)(lb + 4 * b + k) * 8 + u;
+                    const int64_t ve = (int64_t)noff + (int64_t)(vb + 4 * (4 * b + u / 2) + k) * 2 + u % 2;
+                    if (le >= noff + tn || ve >= noff + tn) return "segment leaves its tile";
+                    if (el < rl) {
+                        const int j = rp[r] + el;
+                        const int u_ = P.loff[le] / 256;
+                        const int w = (u_ / 4) / 8, i = (u_ / 4) % 8, qq = u_ % 4;
+                        if (P.tsrc[ve] != j || P.loff[le] == WS_ZOFF || u_ >= nu || g[32 * w + 8 * qq + i] != ci[j])
+                            return "row entry is not its CSR non-zero";
+                    } else if (P.tsrc[ve] != -1 || P.loff[le] != WS_ZOFF) {
+                        return "pad entry does not read the zero row";
+                    }
+                }
+        }
+        return nullptr;
+    };
+    const int nt = P.ntiles;
+    const int nth = std::max(1, std::min({8, (nt + 63) / 64, (int)std::max(1u, std::thread::hardware_concurrency()),
+                                          analysis_threads > 0 ? analysis_threads : 8}));
+    std::vector<const char *> bad((size_t)nth, nullptr);
+    auto work = [&](int w) {
+        for (int t = (int)((int64_t)nt * w / nth); t < (int)((int64_t)nt * (w + 1) / nth) && !bad[(size_t)w]; ++t)
+            bad[(size_t)w] = check_tile(t);
+    };
+    std::vector<std::thread> pool;
+    for (int w = 1; w < nth; ++w) pool.emplace_back(work, w);
+    work(0);
+    for (auto &x : pool) x.join();
+    for (const char *b : bad)
+        if (b) return fail(b);
     return true;
 }
 
@@ -469,9 +497,19 @@ double parts_footprint(int m, int n, const int *rp, const int *ci, const std::ve
 
 bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::string *err, const TileCaps &caps)
 {
+    // SMFV_PLAN_TIMING=1: the phases' host times on stderr (diagnostic)
+    static const bool timing = std::getenv("SMFV_PLAN_TIMING") != nullptr;
+    auto tick = [t = std::chrono::steady_clock::now()](const char *what) mutable {
+        const auto now = std::chrono::steady_clock::now();
+        if (timing)
+            std::fprintf(stderr, "[smfv plan] %s %.1f ms\n", what,
+                         std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    };
     P = WsPlan();
     TileAnalysis T;
     analyse_tiles(m, n, rp, ci, T, caps);  // TileCaps defaults are the k_rows_ws caps
+    tick("analyse_tiles");
 
     auto len8 = [&](int r) { return std::max(8, (rp[r + 1] - rp[r] + 7) & ~7); };
     // the length a team computes: its row's, rounded up to even (the kernel
@@ -484,8 +522,10 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         for (size_t q = 0; q < rows.size(); q += 4) e += 4 * (int64_t)len8(rows[q]);
         return e;
     };
-    std::vector<int> pos((size_t)std::max(n, 1), -1), ucols;
-    auto emit = [&](const std::vector<int> &R) {
+    // one tile into the plan at entry offset noff, record index t (the
+    // tiles are independent: run in parallel, each with its own pos stamps)
+    auto emit = [&](const std::vector<int> &R, int64_t noff, int t, std::vector<int> &pos, std::vector<int> &ucols,
+                    int64_t &tiled, int64_t &unions) {
         ucols.clear();
         for (int r : R)
             for (int j = rp[r]; j < rp[r + 1]; ++j)
@@ -494,16 +534,14 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
                     ucols.push_back(ci[j]);
                 }
         const int nu = (int)ucols.size();
-        const int64_t noff = P.entries;
-        std::vector<int> lrec(WS_LWORDS, 0), grec(WS_GWORDS, 0);
+        int *lrec = &P.lrec[(size_t)t * WS_LWORDS];
+        int *grec = &P.grec[(size_t)t * WS_GWORDS];
         for (int s = 0; s < WS_ROWS; ++s) lrec[s] = -1;
         int64_t e = 0;
         for (int q = 0; 4 * q < (int)R.size(); ++q) {
             const int o = q / 2, w = o < 4 ? o : 11 - o, h = q % 2;  // octet o -> wave; SIMD s runs octets s and 7 - s
             const int nb = len8(R[4 * q]) / 8;
             const int lbase = (int)(e / 8), vbase = (int)(e / 2);
-            P.loff.resize((size_t)(noff + e + 32 * nb), (uint16_t)WS_ZOFF);
-            P.tsrc.resize((size_t)(noff + e + 32 * nb), -1);
             for (int k = 0; k < 4 && 4 * q + k < (int)R.size(); ++k) {
                 const int r = R[4 * q + k], slot = (4 * h + k) * 8 + w;
                 for (int j = rp[r]; j < rp[r + 1]; ++j) {
@@ -515,7 +553,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
                 lrec[slot] = r;
                 lrec[64 + slot] = lbase | (len2(r) << 16);
                 lrec[128 + slot] = vbase;
-                P.tiled_nnz += rp[r + 1] - rp[r];
+                tiled += rp[r + 1] - rp[r];
             }
             e += 32 * nb;
         }
@@ -531,11 +569,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
             grec[WS_G_NU + q] = nu;
         }
         for (int c : ucols) pos[c] = -1;
-        P.grec.insert(P.grec.end(), grec.begin(), grec.end());
-        P.lrec.insert(P.lrec.end(), lrec.begin(), lrec.end());
-        P.entries += e;
-        P.union_rows += nu;
-        ++P.ntiles;
+        unions += nu;
     };
 
     auto by_length = [&](std::vector<int> &R) {
@@ -621,18 +655,45 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         tiles = std::move(out);
         for (int x = 0; x <= 8; ++x) P.xcd[x] = (int)((int64_t)tiles.size() * x / 8);
     }
-    for (auto &R : tiles) {
-        by_length(R);
-        emit(R);
+    tick("split / order tiles");
+    // each tile's entry offset (a prefix sum of its quad layout), then the
+    // tiles emitted in parallel into their own ranges
+    const int nt = (int)tiles.size();
+    std::vector<int64_t> toff((size_t)nt + 1, 0);
+    for (int t = 0; t < nt; ++t) {
+        by_length(tiles[(size_t)t]);
+        toff[(size_t)t + 1] = toff[(size_t)t] + layout(tiles[(size_t)t]);
     }
+    P.ntiles = nt;
+    P.entries = toff[(size_t)nt];
     if (P.entries + WS_SLACK > 0x7fffffff) {
         if (err) *err = "ws plan: too many tile entries for int32 offsets";
         return false;
     }
-    P.loff.resize((size_t)(P.entries + WS_SLACK), (uint16_t)WS_ZOFF);
-    P.tsrc.resize((size_t)(P.entries + WS_SLACK), -1);
+    P.loff.assign((size_t)(P.entries + WS_SLACK), (uint16_t)WS_ZOFF);
+    P.tsrc.assign((size_t)(P.entries + WS_SLACK), -1);
+    P.grec.assign((size_t)nt * WS_GWORDS, 0);
+    P.lrec.assign((size_t)nt * WS_LWORDS, 0);
+    {
+        const int nth = std::max(1, std::min({8, (nt + 63) / 64, (int)std::max(1u, std::thread::hardware_concurrency()),
+                                              analysis_threads > 0 ? analysis_threads : 8}));
+        std::vector<int64_t> tiled((size_t)nth, 0), unions((size_t)nth, 0);
+        auto work = [&](int w) {
+            std::vector<int> pos((size_t)std::max(n, 1), -1), ucols;
+            for (int t = (int)((int64_t)nt * w / nth); t < (int)((int64_t)nt * (w + 1) / nth); ++t)
+                emit(tiles[(size_t)t], toff[(size_t)t], t, pos, ucols, tiled[(size_t)w], unions[(size_t)w]);
+        };
+        std::vector<std::thread> pool;
+        for (int w = 1; w < nth; ++w) pool.emplace_back(work, w);
+        work(0);
+        for (auto &x : pool) x.join();
+        for (int w = 0; w < nth; ++w) P.tiled_nnz += tiled[(size_t)w], P.union_rows += unions[(size_t)w];
+    }
+    tick("emit");
     std::sort(P.direct.begin(), P.direct.end());
-    return verify_ws_plan(m, n, rp, ci, P, err);
+    const bool ok = verify_ws_plan(m, n, rp, ci, P, err);
+    tick("verify");
+    return ok;
 }
 
 // ---------------------------------------------------------------------------
