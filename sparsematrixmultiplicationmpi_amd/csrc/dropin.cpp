@@ -848,10 +848,14 @@ DROPIN_API double smfvDistributeInputs(SparseMatrix &A, FatVector &fat, int k)
         par_rows(n, [&](int64_t a, int64_t b) {
             for (int64_t i = a; i < b; ++i) std::copy(fat[i].begin(), fat[i].end(), hx + (size_t)i * K);
         });
-        hip_check(hipMemcpyAsync(rp, A.rowPtr.data(), ((size_t)m + 1) * sizeof(int), hipMemcpyHostToDevice, st), "H2D");
+        // (through huge-page staging, as a call's uploads: Problem::stage)
+        hip_check(hipMemcpyAsync(rp, Problem::stage(B.hrp, A.rowPtr.data(), ((size_t)m + 1) * sizeof(int)),
+                                 ((size_t)m + 1) * sizeof(int), hipMemcpyHostToDevice, st), "H2D");
         if (nnz) {
-            hip_check(hipMemcpyAsync(ci, A.colIndices.data(), nnz * sizeof(int), hipMemcpyHostToDevice, st), "H2D");
-            hip_check(hipMemcpyAsync(va, A.values.data(), nnz * sizeof(double), hipMemcpyHostToDevice, st), "H2D");
+            hip_check(hipMemcpyAsync(ci, Problem::stage(B.hci, A.colIndices.data(), nnz * sizeof(int)),
+                                     nnz * sizeof(int), hipMemcpyHostToDevice, st), "H2D");
+            hip_check(hipMemcpyAsync(va, Problem::stage(B.hva, A.values.data(), nnz * sizeof(double)),
+                                     nnz * sizeof(double), hipMemcpyHostToDevice, st), "H2D");
         }
         if ((size_t)n * K)
             hip_check(hipMemcpyAsync(X, hx, (size_t)n * K * sizeof(double), hipMemcpyHostToDevice, st), "H2D");
