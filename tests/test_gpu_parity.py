@@ -359,7 +359,21 @@ def test_tiled_plan_stats_cop20k(gpu):
     plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(A, gpu), 32)
     st = plan.stats()
     assert st["reuse"] > 1.9 and st["direct_rows"] == 0
-    assert st["est_reuse"] >= 3.0 and st["tiled"]  # sampled estimate (512 tiles in the full pattern)
+    assert st["est_reuse"] >= 3.0 and st["tiled"]  # sampled estimate (128 tiles in the full pattern)
+    assert st["analysis_ms"] < 2000.0  # ~0.1 s on the box; a generous bound, not a benchmark
+
+
+def test_untiled_pattern_rejected_by_sample(gpu):
+    """A pattern without X-row re-use (uniform random columns) is rejected by
+    the tile sample before any full-pattern pass (parts, footprints): the
+    analysis stays a small fraction of what the r2 order cost (6.3 s on
+    pow10m), so an untiled first call never waits on it."""
+    m = 2_000_000
+    A = smfv.gen_random_rows(m, m, 16.0, 0.0, 16, 11)
+    plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(A, gpu), 32)
+    st = plan.stats()
+    assert not st["tiled"] and st["est_reuse"] < 1.5, st
+    assert st["analysis_ms"] < 1500.0, st
 
 
 def test_dist_rowpart_single_rank(gpu):
