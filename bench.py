@@ -238,6 +238,42 @@ def stream_copy_gbps(dev, nbytes: int = 2 << 30, reps: int = 5) -> float:
     return 2.0 * nbytes / (ms * 1e-3) / 1e9
 
 
+def size_matched_copy(dev, prob_bytes: int, ncopies: int, steps: int, world: int) -> dict | None:
+    """The launch-size floor beside the spec: the same 16-byte non-temporal
+    copy kernel moving the SpMM's algorithmic bytes per launch (half read,
+    half written), rotated over as many buffer pairs as the SpMM's cold
+    copies and timed the same way (one graph of `steps` launches).  Start-up
+    and drain of a ~100 MB launch are in it, as they are in the SpMM's.
+    None where the rotation would not fit comfortably (> 8 GiB)."""
+    import torch
+    from sparsematrixmultiplicationmpi_amd._lib import call
+    half = (prob_bytes // 2) // 16 * 16
+    if half <= 0 or ncopies * 2 * half > (8 << 30):
+        return None
+    bufs = [(torch.empty(half // 8, dtype=torch.float64, device=dev),
+             torch.empty(half // 8, dtype=torch.float64, device=dev)) for _ in range(ncopies)]
+    for a, _ in bufs:
+        a.fill_(1.0)
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g, stream=side):
+            st = torch.cuda.current_stream().cuda_stream
+            for i in range(steps):
+                a, b = bufs[i % ncopies]
+                call("smfv_stream_copy", b.data_ptr(), a.data_ptr(), half, st)
+    torch.cuda.current_stream().wait_stream(side)
+    _stabilize(g)
+    ms = _timed_events(g.replay, world) / steps
+    del g, bufs
+    torch.cuda.empty_cache()
+    return {"bytes_per_launch": 2 * half, "avg_launch_ms": round(ms, 6),
+            "GBps": round(2 * half / (ms * 1e-3) / 1e9, 1),
+            "note": "smfv_stream_copy of the algorithmic bytes per launch, cold rotation, one graph of the "
+                    "timed step count; frac_of_copy_time = copy time / SpMM time"}
+
+
 def _stabilize(g) -> int:
     """Untimed replays of a captured graph for >= STABILIZE_S before its first
     timed region: the GPU's clocks ramp over ~10 ms of load, and one warm
@@ -735,6 +771,8 @@ def main() -> None:
     ap.add_argument("--no-warm", action="store_true",
                     help="skip the same-copy (warm) leg: every launch of the process streams from HBM "
                          "(for a cold-only rocprofv3 kernel trace)")
+    ap.add_argument("--no-copy-floor", action="store_true",
+                    help="skip the size-matched copy (roofline.size_matched_copy)")
     ap.add_argument("--no-check", action="store_true",
                     help="report the post-timing result check but do not fail on it (lab ablations)")
     ap.add_argument("--mfma", action="store_true",
@@ -855,6 +893,7 @@ def main() -> None:
     # leaves it out so a profile of this process holds cold launches only
     span_ms_w = timed(capture(True)) if not args.no_warm else float("nan")
     stream_gbps = stream_copy_gbps(dev)
+    copy_floor = size_matched_copy(dev, prob_bytes, ncopies, args.steps, world) if not args.no_copy_floor else None
     vendor = None
     if variant in ("ROWWISE", "SEQUENTIAL") and not args.no_vendor:
         vendor = vendor_leg(copies, args, timed, 2.0 * nnz * K)
@@ -923,7 +962,9 @@ def main() -> None:
                                                  "min": round(samples[0] / args.steps, 6),
                                                  "max": round(samples[-1] / args.steps, 6)},
                          "stream_copy_GBps": round(stream_gbps, 1),
-                         "frac_of_stream_copy": round(achieved / stream_gbps, 4) if stream_gbps else None},
+                         "frac_of_stream_copy": round(achieved / stream_gbps, 4) if stream_gbps else None,
+                         "size_matched_copy": (dict(copy_floor, frac_of_copy_time=round(copy_floor["avg_launch_ms"] / kern_ms, 4))
+                                               if copy_floor else None)},
             "plan": {"tiled": st["tiled"], "tiles": st["tiles"], "reuse": round(st["reuse"], 3),
                      "est_reuse_sampled": round(st["est_reuse"], 3), "direct_rows": st["direct_rows"],
                      "create_s": round(t_plan[0], 3), "analysis_ms": round(st["analysis_ms"], 1),
