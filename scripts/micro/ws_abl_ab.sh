@@ -12,6 +12,6 @@ done
 for i in $(seq 1 ${ROUNDS:-3}); do
   for abl in ${ABLS:-0 9 10 11}; do
     SMFV_WS_ABL=$abl timeout -k 10 120 python bench.py --no-cpu-baseline --no-vendor ${EXTRA:-} > gpurun_out/r3_ab_abl${abl}_$i.log 2>&1 || exit 3
-    python -c "import json; d=json.loads(open('gpurun_out/r3_ab_abl${abl}_$i.log').read().strip().splitlines()[-1]); print('abl $abl', round(d['ms_per_step']*1000,3), 'us warm', round(d['warm']['avg_launch_ms']*1000,3), d['check']['ok'])"
+    python -c "import json; d=json.loads(open('gpurun_out/r3_ab_abl${abl}_$i.log').read().strip().splitlines()[-1]); print('abl $abl', round(d['ms_per_step']*1000,3), 'us warm', round(d['warm']['avg_launch_ms']*1000,3), d['check']['ok'], 'copy', (d['roofline'].get('size_matched_copy') or {}).get('avg_launch_ms'))"
   done
 done
