@@ -17,7 +17,7 @@ import sys
 pmc_dir, config, ksub, keep = sys.argv[1:5]
 vals = {"FETCH_SIZE": [], "WRITE_SIZE": []}
 kname = None
-for f in glob.glob(f"{pmc_dir}/p*/pmc_counter_collection.csv"):
+for f in glob.glob(f"{pmc_dir}/*/pmc_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
         if ksub in r["Kernel_Name"] and r["Counter_Name"] in vals:
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
@@ -25,7 +25,7 @@ for f in glob.glob(f"{pmc_dir}/p*/pmc_counter_collection.csv"):
 med = {k: sorted(v)[len(v) // 2] for k, v in vals.items()}
 traffic = (2.0 * med["FETCH_SIZE"] + med["WRITE_SIZE"]) * 1024.0
 os.makedirs(keep, exist_ok=True)
-for f in glob.glob(f"{pmc_dir}/p*/pmc_counter_collection.csv"):
+for f in glob.glob(f"{pmc_dir}/*/pmc_counter_collection.csv"):
     shutil.copy(f, os.path.join(keep, os.path.basename(os.path.dirname(f)) + "_counter_collection.csv"))
 path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
 db = json.load(open(path)) if os.path.exists(path) else {}
