@@ -103,7 +103,7 @@ def kernel_label(variant: str, K: int, plan_stats: dict, x_bytes: int = 0) -> st
     if plan_stats.get("mfma"):
         return "k_rows_mfma"
     if plan_stats.get("tiled"):
-        return "k_rows_ws"
+        return "k_spmv_chunks" if K == 1 else "k_rows_ws"
     if K == 1:
         return "k_spmv_stream<256, 64, 2048>"
     if K % 2:

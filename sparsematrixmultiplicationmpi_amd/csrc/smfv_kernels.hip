@@ -259,6 +259,84 @@ __global__ __launch_bounds__(NT) void k_spmv_stream(int row_begin, int nrows, co
     if (t < nr) Y[(int64_t)(lr0 + t) * ldy] = acc;
 }
 
+// ---------------------------------------------------------------------------
+// k_spmv_chunks: K = 1 on a chunk plan (build_spmv_chunks).  Block c owns the
+// rows of chunk c; its CH entry slots start at c * CH, so every lane issues
+// its value (16-B pairs) and column-offset loads (two u16 per dword) at
+// launch, beside the scalar header load, with no row_ptr round trip in
+// front of them.  Lane t holds entries 2 (k NT + t) + {0, 1}: each load
+// instruction of the wave reads one contiguous run.  The products a_j * x_j
+// go to LDS; lane t < rows then adds its row's products in CSR order (the
+// row starts come from the plan), exactly the reference's y += a * x.
+// ---------------------------------------------------------------------------
+typedef double chunk_d2 __attribute__((ext_vector_type(2)));
+constexpr int K1_NT = 256;  // lanes per chunk block = row cap of a chunk
+
+// entry slots per chunk (1,024 or 2,048; lab builds: SMFV_K1_CHUNK)
+static int spmv_chunk_cap()
+{
+#ifdef SMFV_LAB
+    if (const char *e = std::getenv("SMFV_K1_CHUNK")) return std::atoi(e) == 2048 ? 2048 : 1024;
+#endif
+    return 1024;
+}
+
+
+template <int NT, int CH>
+__global__ __launch_bounds__(NT) void k_spmv_chunks(const int4 *__restrict__ hdr, const uint16_t *__restrict__ rs,
+                                                    const uint16_t *__restrict__ off,
+                                                    const double *__restrict__ vals,
+                                                    const double *__restrict__ X, int64_t ldx,
+                                                    double *__restrict__ Y, int64_t ldy)
+{
+    static_assert(CH % (2 * NT) == 0, "whole entry pairs per lane");
+    constexpr int V2 = CH / (2 * NT);
+    __shared__ chunk_d2 prod[CH / 2];
+    const int c = xcd_remap(blockIdx.x, gridDim.x);
+    const int t = threadIdx.x;
+    const int4 h = hdr[c];  // first row, rows, base column, entries (scalar load, in flight with the stream)
+    const chunk_d2 *v2 = reinterpret_cast<const chunk_d2 *>(vals + (int64_t)c * CH);
+    const uint32_t *o2 = reinterpret_cast<const uint32_t *>(off + (int64_t)c * CH);
+    chunk_d2 v[V2];
+    uint32_t o[V2];
+#pragma unroll
+    for (int k = 0; k < V2; ++k) {
+        v[k] = __builtin_nontemporal_load(v2 + k * NT + t);
+        o[k] = __builtin_nontemporal_load(o2 + k * NT + t);
+    }
+    const uint16_t *rsc = rs + (int64_t)c * (NT + 1);
+    const int a = rsc[t], b = rsc[t + 1];
+    // every stream load above is issued before anything waits (the
+    // scheduler would otherwise put some of them behind the header's wait)
+    __builtin_amdgcn_sched_barrier(0);
+    const double *xb = X + (int64_t)h.z * ldx;
+#pragma unroll
+    for (int k = 0; k < V2; ++k) {
+        const double x0 = xb[(int64_t)(o[k] & 0xFFFFu) * ldx];
+        const double x1 = xb[(int64_t)(o[k] >> 16) * ldx];
+        chunk_d2 p;
+        p.x = v[k].x * x0;
+        p.y = v[k].y * x1;
+        prod[k * NT + t] = p;
+    }
+    asm volatile("" ::"v"(a), "v"(b));  // the row starts are loaded now, not after the barrier
+    __syncthreads();
+    if (t < h.y) {
+        const double *pr = reinterpret_cast<const double *>(prod);
+        double acc = 0.0;
+        int j = a;
+        for (; j + 4 <= b; j += 4) {
+            const double p0 = pr[j], p1 = pr[j + 1], p2 = pr[j + 2], p3 = pr[j + 3];
+            acc = acc + p0;
+            acc = acc + p1;
+            acc = acc + p2;
+            acc = acc + p3;
+        }
+        for (; j < b; ++j) acc = acc + pr[j];
+        Y[(int64_t)(h.x + t) * ldy] = acc;
+    }
+}
+
 #ifdef SMFV_LAB
 #include "lab/spmv_lab.inc"  // k_spmv_pipe (lab A/B, measured slower: DESIGN.md section 7)
 #endif
@@ -1522,6 +1600,10 @@ struct smfv_plan_s {
     bool mfma = false;                     // SMFV_PLAN_MFMA: k_rows_mfma (dense blocks) instead of k_rows_ws
     int *mf_rec = nullptr, *mf_ucols = nullptr, *mf_bstep = nullptr;
     uint16_t *ws_loff = nullptr;
+    bool k1 = false;                       // K = 1 chunk plan (k_spmv_chunks), ntiles = chunks
+    int k1_cap = 0;                        // entry slots per chunk
+    int *k1_hdr = nullptr;                 // 4 ints per chunk
+    uint16_t *k1_rs = nullptr, *k1_off = nullptr;
     void *ws = nullptr;
     size_t ws_bytes = 0, dev_bytes = 0;
     hipEvent_t bind_ev = nullptr;          // recorded after the snapshot gather
@@ -1529,7 +1611,8 @@ struct smfv_plan_s {
     ~smfv_plan_s()
     {
         for (void *q : {(void *)tsrc, (void *)tvals, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
-                        (void *)direct_off, (void *)ws_loff, ws, (void *)mf_rec, (void *)mf_ucols, (void *)mf_bstep})
+                        (void *)direct_off, (void *)ws_loff, ws, (void *)mf_rec, (void *)mf_ucols, (void *)mf_bstep,
+                        (void *)k1_hdr, (void *)k1_rs, (void *)k1_off})
             if (q) (void)hipFree(q);
         if (bind_ev) (void)hipEventDestroy(bind_ev);
     }
@@ -1686,6 +1769,34 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                         p->dev_bytes += b;
                     }
                 }
+            }
+        }
+    }
+    // K = 1: the chunk plan (k_spmv_chunks) wherever the pattern fits its
+    // layout (no row over a chunk, 16-bit column spans); otherwise the plan
+    // stays untiled (k_spmv_stream on the live CSR)
+    if (!rc && whole_rows && h_rp && h_ci && m > 0 && K == 1 && !(flags & (SMFV_PLAN_NO_TILES | SMFV_PLAN_MFMA))) {
+        std::vector<int> rpl((size_t)m + 1);
+        for (int i = 0; i <= m; ++i) rpl[i] = (int)(h_rp[row_begin + i] - nnz_base);
+        SpmvChunkPlan C;
+        std::string err;
+        if (build_spmv_chunks(m, n, rpl.data(), h_ci + nnz_base, spmv_chunk_cap(), K1_NT, C, &err)) {
+            p->tiled = p->k1 = true;
+            p->k1_cap = C.cap;
+            p->ntiles = C.nchunks;
+            p->tiled_nnz = C.entries;
+            p->padded_nnz = (int64_t)C.nchunks * C.cap;
+            for (int &q : C.tsrc)
+                if (q >= 0) q += (int)nnz_base;
+            p->snapshot = (int64_t)C.tsrc.size();
+            if (!rc) rc = upload(&p->k1_hdr, C.hdr, p->dev_bytes);
+            if (!rc) rc = upload(&p->k1_rs, C.rs, p->dev_bytes);
+            if (!rc) rc = upload(&p->k1_off, C.off, p->dev_bytes);
+            if (!rc) rc = upload(&p->tsrc, C.tsrc, p->dev_bytes);
+            if (!rc) {
+                const size_t b = std::max<size_t>((size_t)p->snapshot, 1) * sizeof(double);
+                fail_hip(hipMalloc(reinterpret_cast<void **>(&p->tvals), b), "hipMalloc(tvals)");
+                p->dev_bytes += b;
             }
         }
     }
@@ -1887,7 +1998,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     SMFV_REQUIRE(d_row_ptr && d_Y, "null row_ptr / Y");
     SMFV_REQUIRE(plan->nnz == 0 || (d_col_idx && d_values && d_X), "null col_idx / values / X");
     hipStream_t st = as_stream(stream);
-    if (!plan->tiled || pick_vec(d_X, ldx, d_Y, ldy, K) != 2) {
+    if (!plan->tiled || (!plan->k1 && pick_vec(d_X, ldx, d_Y, ldy, K) != 2)) {
         // untiled: the row / merge kernels on the live values
         if (plan->variant == SMFV_NONZERO)
             return launch_merge(plan->row_begin, m, plan->nnz_base, plan->nnz_end, d_row_ptr, d_col_idx, d_values,
@@ -1911,6 +2022,16 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
                       "capturing; synchronize the bind stream before capture");
             return SMFV_ERR_INVALID;
         }
+    }
+    if (plan->k1) {
+        if (plan->ntiles > 0) {
+            auto kern = plan->k1_cap == 2048 ? k_spmv_chunks<K1_NT, 2048> : k_spmv_chunks<K1_NT, 1024>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)plan->ntiles), dim3(K1_NT), 0, st,
+                               reinterpret_cast<const int4 *>(plan->k1_hdr), plan->k1_rs, plan->k1_off, plan->tvals,
+                               d_X, ldx, d_Y, ldy);
+            SMFV_LAUNCHED();
+        }
+        return SMFV_OK;
     }
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess) {

@@ -778,4 +778,89 @@ bool build_mfma_plan(int m, int n, const int *rp, const int *ci, MfmaPlan &P, st
     return true;
 }
 
+bool build_spmv_chunks(int m, int n, const int *rp, const int *ci, int cap, int maxrows, SpmvChunkPlan &P,
+                       std::string *err)
+{
+    auto fail = [&](const char *what, long long a) {
+        if (err) {
+            char b[160];
+            std::snprintf(b, sizeof b, "spmv chunk plan: %s (%lld)", what, a);
+            *err = b;
+        }
+        return false;
+    };
+    if (cap <= 0 || cap > 65535 || maxrows <= 0 || maxrows > cap) return fail("bad caps", cap);
+    P = SpmvChunkPlan();
+    P.cap = cap;
+    P.maxrows = maxrows;
+    // greedy packing in row order: a chunk ends when the next row would pass
+    // the entry cap, the row cap or the 16-bit column span
+    std::vector<int> first;
+    std::vector<int> base;
+    int r = 0;
+    while (r < m) {
+        const int r0 = r;
+        int lo = n, hi = -1, cnt = 0;
+        while (r < m && r - r0 < maxrows) {
+            const int len = rp[r + 1] - rp[r];
+            if (len > cap) return fail("row longer than a chunk", r);
+            int rlo = lo, rhi = hi;
+            for (int j = rp[r]; j < rp[r + 1]; ++j) rlo = std::min(rlo, ci[j]), rhi = std::max(rhi, ci[j]);
+            if (len > 0 && rhi - rlo > 65535) {
+                if (r == r0) return fail("row columns span more than 16 bits", r);
+                break;
+            }
+            if (cnt + len > cap) break;
+            lo = rlo, hi = rhi, cnt += len, ++r;
+        }
+        first.push_back(r0);
+        base.push_back(hi >= 0 ? lo : 0);
+    }
+    first.push_back(m);
+    const int nc = (int)base.size();
+    P.nchunks = nc;
+    P.hdr.assign((size_t)nc * 4, 0);
+    P.rs.assign((size_t)nc * (maxrows + 1), 0);
+    P.off.assign((size_t)nc * cap, 0);
+    P.tsrc.assign((size_t)nc * cap, -1);
+    for (int c = 0; c < nc; ++c) {
+        const int r0 = first[c], nr = first[c + 1] - r0;
+        int e = 0;
+        for (int t = 0; t < nr; ++t) {
+            P.rs[(size_t)c * (maxrows + 1) + t] = (uint16_t)e;
+            for (int j = rp[r0 + t]; j < rp[r0 + t + 1]; ++j, ++e) {
+                P.off[(size_t)c * cap + e] = (uint16_t)(ci[j] - base[c]);
+                P.tsrc[(size_t)c * cap + e] = j;
+            }
+        }
+        for (int t = nr; t <= maxrows; ++t) P.rs[(size_t)c * (maxrows + 1) + t] = (uint16_t)e;
+        int *h = &P.hdr[(size_t)c * 4];
+        h[0] = r0, h[1] = nr, h[2] = base[c], h[3] = e;
+        P.entries += e;
+    }
+    // replay the kernel's reads: every row once, in order, each entry's value
+    // index and column as CSR has them
+    int next = 0;
+    for (int c = 0; c < nc; ++c) {
+        const int *h = &P.hdr[(size_t)c * 4];
+        if (h[0] != next || h[1] < 0 || h[1] > maxrows || h[3] > cap) return fail("chunk header", c);
+        const uint16_t *s = &P.rs[(size_t)c * (maxrows + 1)];
+        for (int t = 0; t < h[1]; ++t) {
+            const int r = h[0] + t;
+            if (s[t + 1] - s[t] != rp[r + 1] - rp[r]) return fail("row length", r);
+            for (int k = s[t]; k < s[t + 1]; ++k) {
+                const size_t slot = (size_t)c * cap + k;
+                const int j = rp[r] + (k - s[t]);
+                if (P.tsrc[slot] != j || h[2] + P.off[slot] != ci[j]) return fail("entry", j);
+            }
+        }
+        if (s[h[1]] != h[3]) return fail("chunk entry count", c);
+        for (int k = h[3]; k < cap; ++k)
+            if (P.tsrc[(size_t)c * cap + k] != -1 || P.off[(size_t)c * cap + k] != 0) return fail("pad", c);
+        next = h[0] + h[1];
+    }
+    if (next != m || P.entries != (m ? (int64_t)rp[m] - rp[0] : 0)) return fail("rows not covered", next);
+    return true;
+}
+
 }  // namespace smfv

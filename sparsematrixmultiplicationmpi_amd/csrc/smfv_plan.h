@@ -169,4 +169,26 @@ struct MfmaPlan {
 bool build_mfma_plan(int m, int n, const int *row_ptr, const int *col_idx, MfmaPlan &out, std::string *err,
                      const TileCaps &caps = TileCaps());
 
+// K = 1 chunk plan (k_spmv_chunks, the SpMV of BASELINE config 1 on the GPU).
+// Consecutive rows are packed into chunks of at most `cap` non-zeros and
+// `maxrows` rows; chunk c's entries sit at slots [c * cap, c * cap + count)
+// in CSR order, so a block streams its chunk from an address it knows at
+// launch (no row_ptr round trip first) and sums each row in CSR order from
+// LDS (bit-identical to SC/SparseMatrixFatVectorMultiply.cpp:17-27 at K = 1).
+// Each entry carries its column as a 16-bit offset from the chunk's lowest
+// column: 10 bytes per entry with the values snapshot, against CSR's 12.
+struct SpmvChunkPlan {
+    int nchunks = 0, cap = 0, maxrows = 0;
+    std::vector<int> hdr;        // 4 per chunk: first row, rows, base column, entries
+    std::vector<uint16_t> rs;    // maxrows + 1 per chunk: row starts in the chunk (entry `rows` = entries)
+    std::vector<uint16_t> off;   // cap per chunk: column - base column (pads 0)
+    std::vector<int> tsrc;       // cap per chunk: CSR index of the entry's value (-1: pad)
+    int64_t entries = 0;         // non-zeros placed (= nnz of the block)
+};
+// false (with *err saying why) when the pattern does not fit the layout: a
+// row longer than cap, or a row whose columns span more than 65,535.  The
+// plan is verified by replaying the kernel's reads before it is returned.
+bool build_spmv_chunks(int m, int n, const int *row_ptr, const int *col_idx, int cap, int maxrows,
+                       SpmvChunkPlan &out, std::string *err);
+
 }  // namespace smfv

@@ -496,6 +496,81 @@ def test_spmv_stream_k1(gpu):
     assert np.array_equal(bits(Y[250:650].cpu().numpy()), bits(Yref[250:650]))
 
 
+def _chunk_matrix(seed, m=9000, n=200000):
+    """Rows for the K = 1 chunk plan's edges: empty rows, runs of 300 short
+    rows (more rows than a chunk's 256 lanes), rows of exactly 1,024 and
+    1,023 entries (a whole chunk), a sliding column band (every row spans
+    < 2^16) that jumps back for rows 6000-6009 (chunks end on the span)."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 48, m)
+    lens[100:400] = rng.integers(0, 3, 300)
+    lens[[0, 1, 2, m - 1]] = 0
+    lens[[500, 501, 4000]] = [1024, 1023, 1024]
+    rp = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    ci = []
+    for r, L in enumerate(lens):
+        lo = 0 if 6000 <= r < 6010 else r * (n - 60000) // m
+        ci.append(np.sort(rng.choice(np.arange(lo, lo + 60000), L, replace=False)))
+    return mat(rp, np.concatenate(ci).astype(np.int32), rng.uniform(-1, 1, rp[-1]), m, n)
+
+
+def test_spmv_chunk_plan_k1(gpu):
+    """K = 1 plans take the chunk layout (k_spmv_chunks: 16-bit column
+    offsets, values snapshot, no row_ptr round trip) wherever the pattern
+    fits it -- bit-identical to the reference's sequential sum for every
+    variant, unaligned leading dimensions, row blocks and after an in-place
+    value change; a row longer than a chunk or spanning more than 2^16
+    columns keeps the plan on k_spmv_stream."""
+    A = _chunk_matrix(61)
+    X = np.random.default_rng(62).uniform(-1, 1, (A.numCols, 1))
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    dA = smfv.DeviceCSR(A, gpu)
+    dX = torch.from_numpy(X).to(gpu)
+    for v in (smfv.Variant.ROWWISE, smfv.Variant.COLUMNWISE, smfv.Variant.NONZERO):
+        plan = smfv.SpmmPlan(v, dA, 1)
+        st = plan.stats()
+        assert st["tiled"] and st["tiles"] >= A.nnz // 2048, (v, st)
+        for pads in ((0, 0), (1, 3)):
+            Xb = torch.zeros((A.numCols, 1 + pads[0]), dtype=torch.float64, device=gpu)
+            Xb[:, :1] = dX
+            Yb = torch.full((A.numRows, 1 + pads[1]), np.nan, dtype=torch.float64, device=gpu)
+            plan.run(Xb[:, :1], Yb[:, :1])
+            torch.cuda.synchronize()
+            assert np.array_equal(bits(Yb[:, :1].cpu().numpy()), bits(Yref)), (v, pads)
+            if pads[1]:
+                assert torch.isnan(Yb[:, 1:]).all()
+    for r0, r1 in ((0, 9000), (450, 4100), (8990, 9000), (77, 77)):
+        plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, 1, rows=(r0, r1))
+        Y = torch.full((r1 - r0, 1), np.nan, dtype=torch.float64, device=gpu)
+        plan.run(dX, Y)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref[r0:r1])), (r0, r1, plan.stats())
+        assert plan.stats()["tiled"] == (r1 > r0)
+    # the matrix's cached plan re-binds after an in-place value change
+    Y = torch.empty((A.numRows, 1), dtype=torch.float64, device=gpu)
+    S.spmm(smfv.Variant.ROWWISE, dA, dX, Y)
+    dA.values.mul_(-3.0)
+    S.spmm(smfv.Variant.ROWWISE, dA, dX, Y)
+    torch.cuda.synchronize()
+    Y3 = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values * -3.0, X)
+    assert np.array_equal(bits(Y.cpu().numpy()), bits(Y3))
+    # patterns outside the layout stay on the untiled SpMV kernel
+    rp = np.array([0, 3, 1503, 1506], np.int32)
+    wide = mat(rp, np.concatenate([[0, 1, 2], np.arange(1500) * 3, [5, 70000, 70001]]).astype(np.int32),
+               np.random.default_rng(63).uniform(-1, 1, 1506), 3, 80000)
+    long_row = mat(np.array([0, 1100], np.int32), np.arange(1100, dtype=np.int32),
+                   np.random.default_rng(64).uniform(-1, 1, 1100), 1, 2000)
+    for B in (wide, long_row):
+        XB = np.random.default_rng(65).uniform(-1, 1, (B.numCols, 1))
+        plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(B, gpu), 1)
+        assert not plan.stats()["tiled"]
+        Y = torch.empty((B.numRows, 1), dtype=torch.float64, device=gpu)
+        plan.run(torch.from_numpy(XB).to(gpu), Y)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(Y.cpu().numpy()), bits(oracle.spmm("sequential", B.rowPtr, B.colIndices,
+                                                                       B.values, XB)))
+
+
 def _forced_plan_matrix(seed):
     """fem27 rows plus a few rows too wide for a tile (direct rows)."""
     A = smfv.gen_random_rows(6000, 5000, 16, 2.0, 1500, seed)
