@@ -116,12 +116,18 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz,
  * stages each tile's X rows once and reads them from LDS -- same per-row
  * order and arithmetic, bit-identical result; rows over a cap alone are
  * gathered straight from X by a second launch.  Tiling is used when the
- * re-use (non-zeros per staged X row) is >= 3 -- estimated first on 512 tiles
+ * re-use (non-zeros per staged X row) is >= 3 -- estimated first on 128 tiles
  * grown in the full pattern, so the decision does not depend on the row
  * numbering -- or when SMFV_PLAN_FORCE_TILES is set.  A NONZERO plan over
  * whole rows takes the same tiled kernel under the same rule (bit-identical
  * to the reference's NonZeroElement with one rank, which sums every row in
  * CSR order); otherwise, and with SMFV_PLAN_NO_TILES, it runs the merge path.
+ * With K == 1 (SpMV) a plan over whole rows takes the chunk layout of
+ * k_spmv_chunks wherever the pattern fits it (smfv_spmv_chunks_analyse):
+ * consecutive rows packed into 1,024-entry chunks at fixed addresses, the
+ * values snapshot and 16-bit column offsets (10 B per entry against CSR's
+ * 12; 32-bit columns where a row spans more than 65,535 columns); it is a
+ * tiled plan for the values contract below.
  *
  * Values contract of a TILED plan: smfv_plan_bind_values gathers a snapshot
  * of A's device values (tile order, and the directly-gathered rows) and the
@@ -201,6 +207,16 @@ SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_
  * reads, summed, over the block's distinct X rows).  No device needed. */
 SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int *h_row_ptr,
                                     const int *h_col_idx, int flags, double out[9]);
+/* The K = 1 chunk layout (k_spmv_chunks) of the row block [row_begin,
+ * row_end) with `cap` entry slots per chunk (1024 or 2048; 0: the plans'
+ * default), built and verified as smfv_plan_create builds it for K = 1:
+ * out[0] 1 if the pattern fits the layout (else 0: a row longer than a
+ * chunk), [1] chunks, [2] non-zeros placed, [3] most rows in a chunk, [4]
+ * mean fill of a chunk's slots, [5] 1 for the wide layout (32-bit columns:
+ * some row spans more than 65,535 columns), 0 for 16-bit offsets.  No device
+ * needed.  (SC/SparseMatrixFatVectorMultiply.cpp:17-27 at vecCols = 1.) */
+SMFV_API int smfv_spmv_chunks_analyse(int row_begin, int row_end, int n, const int *h_row_ptr,
+                                      const int *h_col_idx, int cap, double out[6]);
 SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int *d_col_idx,
                                const double *d_values, const double *d_X, int64_t ldx,
                                double *d_Y, int64_t ldy, void *stream);

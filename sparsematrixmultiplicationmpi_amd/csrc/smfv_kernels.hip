@@ -282,9 +282,9 @@ static int spmv_chunk_cap()
 }
 
 
-template <int NT, int CH>
+template <int NT, int CH, bool WIDE>
 __global__ __launch_bounds__(NT) void k_spmv_chunks(const int4 *__restrict__ hdr, const uint16_t *__restrict__ rs,
-                                                    const uint16_t *__restrict__ off,
+                                                    const uint16_t *__restrict__ off, const int *__restrict__ col,
                                                     const double *__restrict__ vals,
                                                     const double *__restrict__ X, int64_t ldx,
                                                     double *__restrict__ Y, int64_t ldy)
@@ -297,12 +297,18 @@ __global__ __launch_bounds__(NT) void k_spmv_chunks(const int4 *__restrict__ hdr
     const int4 h = hdr[c];  // first row, rows, base column, entries (scalar load, in flight with the stream)
     const chunk_d2 *v2 = reinterpret_cast<const chunk_d2 *>(vals + (int64_t)c * CH);
     const uint32_t *o2 = reinterpret_cast<const uint32_t *>(off + (int64_t)c * CH);
+    const uint64_t *c2 = reinterpret_cast<const uint64_t *>(col + (int64_t)c * CH);
     chunk_d2 v[V2];
     uint32_t o[V2];
+    uint64_t cc[V2];
 #pragma unroll
     for (int k = 0; k < V2; ++k) {
         v[k] = __builtin_nontemporal_load(v2 + k * NT + t);
-        o[k] = __builtin_nontemporal_load(o2 + k * NT + t);
+        if constexpr (WIDE) {
+            cc[k] = __builtin_nontemporal_load(c2 + k * NT + t);  // two 32-bit columns
+        } else {
+            o[k] = __builtin_nontemporal_load(o2 + k * NT + t);
+        }
     }
     const uint16_t *rsc = rs + (int64_t)c * (NT + 1);
     const int a = rsc[t], b = rsc[t + 1];
@@ -312,8 +318,10 @@ __global__ __launch_bounds__(NT) void k_spmv_chunks(const int4 *__restrict__ hdr
     const double *xb = X + (int64_t)h.z * ldx;
 #pragma unroll
     for (int k = 0; k < V2; ++k) {
-        const double x0 = xb[(int64_t)(o[k] & 0xFFFFu) * ldx];
-        const double x1 = xb[(int64_t)(o[k] >> 16) * ldx];
+        const int64_t j0 = WIDE ? (int64_t)(int)(uint32_t)cc[k] : (int64_t)(o[k] & 0xFFFFu);
+        const int64_t j1 = WIDE ? (int64_t)(int)(uint32_t)(cc[k] >> 32) : (int64_t)(o[k] >> 16);
+        const double x0 = xb[j0 * ldx];
+        const double x1 = xb[j1 * ldx];
         chunk_d2 p;
         p.x = v[k].x * x0;
         p.y = v[k].y * x1;
@@ -1604,6 +1612,8 @@ struct smfv_plan_s {
     int k1_cap = 0;                        // entry slots per chunk
     int *k1_hdr = nullptr;                 // 4 ints per chunk
     uint16_t *k1_rs = nullptr, *k1_off = nullptr;
+    int *k1_col = nullptr;                 // wide layout: 32-bit columns (k1_off unused)
+    bool k1_wide = false;
     void *ws = nullptr;
     size_t ws_bytes = 0, dev_bytes = 0;
     hipEvent_t bind_ev = nullptr;          // recorded after the snapshot gather
@@ -1612,7 +1622,7 @@ struct smfv_plan_s {
     {
         for (void *q : {(void *)tsrc, (void *)tvals, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
                         (void *)direct_off, (void *)ws_loff, ws, (void *)mf_rec, (void *)mf_ucols, (void *)mf_bstep,
-                        (void *)k1_hdr, (void *)k1_rs, (void *)k1_off})
+                        (void *)k1_hdr, (void *)k1_rs, (void *)k1_off, (void *)k1_col})
             if (q) (void)hipFree(q);
         if (bind_ev) (void)hipEventDestroy(bind_ev);
     }
@@ -1783,6 +1793,7 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
         if (build_spmv_chunks(m, n, rpl.data(), h_ci + nnz_base, spmv_chunk_cap(), K1_NT, C, &err)) {
             p->tiled = p->k1 = true;
             p->k1_cap = C.cap;
+            p->k1_wide = C.wide;
             p->ntiles = C.nchunks;
             p->tiled_nnz = C.entries;
             p->padded_nnz = (int64_t)C.nchunks * C.cap;
@@ -1791,7 +1802,7 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
             p->snapshot = (int64_t)C.tsrc.size();
             if (!rc) rc = upload(&p->k1_hdr, C.hdr, p->dev_bytes);
             if (!rc) rc = upload(&p->k1_rs, C.rs, p->dev_bytes);
-            if (!rc) rc = upload(&p->k1_off, C.off, p->dev_bytes);
+            if (!rc) rc = C.wide ? upload(&p->k1_col, C.col, p->dev_bytes) : upload(&p->k1_off, C.off, p->dev_bytes);
             if (!rc) rc = upload(&p->tsrc, C.tsrc, p->dev_bytes);
             if (!rc) {
                 const size_t b = std::max<size_t>((size_t)p->snapshot, 1) * sizeof(double);
@@ -1928,6 +1939,31 @@ SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int
     return SMFV_OK;
 }
 
+SMFV_API int smfv_spmv_chunks_analyse(int row_begin, int row_end, int n, const int *h_row_ptr_all,
+                                      const int *h_col_idx_all, int cap, double out[6])
+{
+    SMFV_REQUIRE(row_begin >= 0 && row_end >= row_begin && n >= 0 && h_row_ptr_all && out &&
+                     (h_row_ptr_all[row_end] == h_row_ptr_all[row_begin] || h_col_idx_all),
+                 "bad argument");
+    SMFV_REQUIRE(cap == 0 || cap == 1024 || cap == 2048, "chunk cap must be 1024 or 2048");
+    const int m = row_end - row_begin, base = h_row_ptr_all[row_begin];
+    std::vector<int> rpl((size_t)m + 1);
+    for (int i = 0; i <= m; ++i) rpl[i] = h_row_ptr_all[row_begin + i] - base;
+    SpmvChunkPlan C;
+    std::string err;
+    const bool fits = build_spmv_chunks(m, n, rpl.data(), h_col_idx_all ? h_col_idx_all + base : nullptr,
+                                        cap ? cap : spmv_chunk_cap(), K1_NT, C, &err);
+    int most = 0;
+    for (int c = 0; c < C.nchunks && fits; ++c) most = std::max(most, C.hdr[(size_t)c * 4 + 1]);
+    out[0] = fits ? 1.0 : 0.0;
+    out[1] = fits ? C.nchunks : 0;
+    out[2] = fits ? (double)C.entries : 0.0;
+    out[3] = most;
+    out[4] = fits && C.nchunks ? (double)C.entries / ((double)C.nchunks * C.cap) : 0.0;
+    out[5] = fits && C.wide ? 1.0 : 0.0;
+    return SMFV_OK;
+}
+
 SMFV_API void smfv_set_analysis_threads(int threads) { smfv::analysis_threads = threads > 0 ? threads : 0; }
 
 SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, void *stream)
@@ -2025,10 +2061,13 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     }
     if (plan->k1) {
         if (plan->ntiles > 0) {
-            auto kern = plan->k1_cap == 2048 ? k_spmv_chunks<K1_NT, 2048> : k_spmv_chunks<K1_NT, 1024>;
+            auto kern = plan->k1_wide ? (plan->k1_cap == 2048 ? k_spmv_chunks<K1_NT, 2048, true>
+                                                              : k_spmv_chunks<K1_NT, 1024, true>)
+                                      : (plan->k1_cap == 2048 ? k_spmv_chunks<K1_NT, 2048, false>
+                                                              : k_spmv_chunks<K1_NT, 1024, false>);
             hipLaunchKernelGGL(kern, dim3((unsigned)plan->ntiles), dim3(K1_NT), 0, st,
-                               reinterpret_cast<const int4 *>(plan->k1_hdr), plan->k1_rs, plan->k1_off, plan->tvals,
-                               d_X, ldx, d_Y, ldy);
+                               reinterpret_cast<const int4 *>(plan->k1_hdr), plan->k1_rs, plan->k1_off, plan->k1_col,
+                               plan->tvals, d_X, ldx, d_Y, ldy);
             SMFV_LAUNCHED();
         }
         return SMFV_OK;

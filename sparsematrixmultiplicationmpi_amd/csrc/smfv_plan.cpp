@@ -779,7 +779,7 @@ bool build_mfma_plan(int m, int n, const int *rp, const int *ci, MfmaPlan &P, st
 }
 
 bool build_spmv_chunks(int m, int n, const int *rp, const int *ci, int cap, int maxrows, SpmvChunkPlan &P,
-                       std::string *err)
+                       std::string *err, bool allow_wide)
 {
     auto fail = [&](const char *what, long long a) {
         if (err) {
@@ -793,8 +793,17 @@ bool build_spmv_chunks(int m, int n, const int *rp, const int *ci, int cap, int 
     P = SpmvChunkPlan();
     P.cap = cap;
     P.maxrows = maxrows;
+    for (int r = 0; r < m; ++r) {
+        if (rp[r + 1] - rp[r] > cap) return fail("row longer than a chunk", r);
+        if (rp[r + 1] > rp[r]) {
+            int lo = n, hi = -1;
+            for (int j = rp[r]; j < rp[r + 1]; ++j) lo = std::min(lo, ci[j]), hi = std::max(hi, ci[j]);
+            if (hi - lo > 65535) P.wide = true;
+        }
+    }
+    if (P.wide && !allow_wide) return fail("row columns span more than 16 bits", 0);
     // greedy packing in row order: a chunk ends when the next row would pass
-    // the entry cap, the row cap or the 16-bit column span
+    // the entry cap, the row cap or (narrow layout) the 16-bit column span
     std::vector<int> first;
     std::vector<int> base;
     int r = 0;
@@ -803,13 +812,10 @@ bool build_spmv_chunks(int m, int n, const int *rp, const int *ci, int cap, int 
         int lo = n, hi = -1, cnt = 0;
         while (r < m && r - r0 < maxrows) {
             const int len = rp[r + 1] - rp[r];
-            if (len > cap) return fail("row longer than a chunk", r);
             int rlo = lo, rhi = hi;
-            for (int j = rp[r]; j < rp[r + 1]; ++j) rlo = std::min(rlo, ci[j]), rhi = std::max(rhi, ci[j]);
-            if (len > 0 && rhi - rlo > 65535) {
-                if (r == r0) return fail("row columns span more than 16 bits", r);
-                break;
-            }
+            if (!P.wide)
+                for (int j = rp[r]; j < rp[r + 1]; ++j) rlo = std::min(rlo, ci[j]), rhi = std::max(rhi, ci[j]);
+            if (len > 0 && rhi - rlo > 65535) break;  // (narrow only; never the chunk's first row)
             if (cnt + len > cap) break;
             lo = rlo, hi = rhi, cnt += len, ++r;
         }
@@ -821,7 +827,10 @@ bool build_spmv_chunks(int m, int n, const int *rp, const int *ci, int cap, int 
     P.nchunks = nc;
     P.hdr.assign((size_t)nc * 4, 0);
     P.rs.assign((size_t)nc * (maxrows + 1), 0);
-    P.off.assign((size_t)nc * cap, 0);
+    if (P.wide)
+        P.col.assign((size_t)nc * cap, 0);
+    else
+        P.off.assign((size_t)nc * cap, 0);
     P.tsrc.assign((size_t)nc * cap, -1);
     for (int c = 0; c < nc; ++c) {
         const int r0 = first[c], nr = first[c + 1] - r0;
@@ -829,7 +838,10 @@ bool build_spmv_chunks(int m, int n, const int *rp, const int *ci, int cap, int 
         for (int t = 0; t < nr; ++t) {
             P.rs[(size_t)c * (maxrows + 1) + t] = (uint16_t)e;
             for (int j = rp[r0 + t]; j < rp[r0 + t + 1]; ++j, ++e) {
-                P.off[(size_t)c * cap + e] = (uint16_t)(ci[j] - base[c]);
+                if (P.wide)
+                    P.col[(size_t)c * cap + e] = ci[j];
+                else
+                    P.off[(size_t)c * cap + e] = (uint16_t)(ci[j] - base[c]);
                 P.tsrc[(size_t)c * cap + e] = j;
             }
         }
@@ -851,12 +863,15 @@ bool build_spmv_chunks(int m, int n, const int *rp, const int *ci, int cap, int 
             for (int k = s[t]; k < s[t + 1]; ++k) {
                 const size_t slot = (size_t)c * cap + k;
                 const int j = rp[r] + (k - s[t]);
-                if (P.tsrc[slot] != j || h[2] + P.off[slot] != ci[j]) return fail("entry", j);
+                const int col = P.wide ? P.col[slot] : h[2] + P.off[slot];
+                if (P.tsrc[slot] != j || col != ci[j]) return fail("entry", j);
             }
         }
         if (s[h[1]] != h[3]) return fail("chunk entry count", c);
-        for (int k = h[3]; k < cap; ++k)
-            if (P.tsrc[(size_t)c * cap + k] != -1 || P.off[(size_t)c * cap + k] != 0) return fail("pad", c);
+        for (int k = h[3]; k < cap; ++k) {
+            const size_t slot = (size_t)c * cap + k;
+            if (P.tsrc[slot] != -1 || (P.wide ? P.col[slot] : P.off[slot]) != 0) return fail("pad", c);
+        }
         next = h[0] + h[1];
     }
     if (next != m || P.entries != (m ? (int64_t)rp[m] - rp[0] : 0)) return fail("rows not covered", next);

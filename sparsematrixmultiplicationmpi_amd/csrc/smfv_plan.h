@@ -176,19 +176,25 @@ bool build_mfma_plan(int m, int n, const int *row_ptr, const int *col_idx, MfmaP
 // launch (no row_ptr round trip first) and sums each row in CSR order from
 // LDS (bit-identical to SC/SparseMatrixFatVectorMultiply.cpp:17-27 at K = 1).
 // Each entry carries its column as a 16-bit offset from the chunk's lowest
-// column: 10 bytes per entry with the values snapshot, against CSR's 12.
+// column (10 bytes per entry with the values snapshot, against CSR's 12);
+// a pattern with a row whose columns span more than 65,535 takes the wide
+// layout instead (32-bit columns, 12 bytes per entry, still streamed from
+// fixed addresses).
 struct SpmvChunkPlan {
     int nchunks = 0, cap = 0, maxrows = 0;
-    std::vector<int> hdr;        // 4 per chunk: first row, rows, base column, entries
+    bool wide = false;           // 32-bit columns in `col` (else 16-bit offsets in `off`)
+    std::vector<int> hdr;        // 4 per chunk: first row, rows, base column (0 if wide), entries
     std::vector<uint16_t> rs;    // maxrows + 1 per chunk: row starts in the chunk (entry `rows` = entries)
-    std::vector<uint16_t> off;   // cap per chunk: column - base column (pads 0)
+    std::vector<uint16_t> off;   // cap per chunk: column - base column (pads 0); narrow layout
+    std::vector<int> col;        // cap per chunk: column (pads 0); wide layout
     std::vector<int> tsrc;       // cap per chunk: CSR index of the entry's value (-1: pad)
     int64_t entries = 0;         // non-zeros placed (= nnz of the block)
 };
 // false (with *err saying why) when the pattern does not fit the layout: a
-// row longer than cap, or a row whose columns span more than 65,535.  The
-// plan is verified by replaying the kernel's reads before it is returned.
+// row longer than cap (or, with allow_wide false, a row whose columns span
+// more than 65,535).  The plan is verified by replaying the kernel's reads
+// before it is returned.
 bool build_spmv_chunks(int m, int n, const int *row_ptr, const int *col_idx, int cap, int maxrows,
-                       SpmvChunkPlan &out, std::string *err);
+                       SpmvChunkPlan &out, std::string *err, bool allow_wide = true);
 
 }  // namespace smfv

@@ -519,8 +519,8 @@ def test_spmv_chunk_plan_k1(gpu):
     offsets, values snapshot, no row_ptr round trip) wherever the pattern
     fits it -- bit-identical to the reference's sequential sum for every
     variant, unaligned leading dimensions, row blocks and after an in-place
-    value change; a row longer than a chunk or spanning more than 2^16
-    columns keeps the plan on k_spmv_stream."""
+    value change; a row spanning more than 2^16 columns switches the plan to
+    32-bit columns, a row longer than a chunk keeps it on k_spmv_stream."""
     A = _chunk_matrix(61)
     X = np.random.default_rng(62).uniform(-1, 1, (A.numCols, 1))
     Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
@@ -554,16 +554,16 @@ def test_spmv_chunk_plan_k1(gpu):
     torch.cuda.synchronize()
     Y3 = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values * -3.0, X)
     assert np.array_equal(bits(Y.cpu().numpy()), bits(Y3))
-    # patterns outside the layout stay on the untiled SpMV kernel
-    rp = np.array([0, 3, 1503, 1506], np.int32)
-    wide = mat(rp, np.concatenate([[0, 1, 2], np.arange(1500) * 3, [5, 70000, 70001]]).astype(np.int32),
-               np.random.default_rng(63).uniform(-1, 1, 1506), 3, 80000)
+    # a row spanning > 2^16 columns: the wide layout; a row over a chunk: untiled
+    rp = np.array([0, 3, 1003, 1006], np.int32)
+    wide = mat(rp, np.concatenate([[0, 1, 2], np.arange(1000) * 79, [5, 70000, 70001]]).astype(np.int32),
+               np.random.default_rng(63).uniform(-1, 1, 1006), 3, 80000)
     long_row = mat(np.array([0, 1100], np.int32), np.arange(1100, dtype=np.int32),
                    np.random.default_rng(64).uniform(-1, 1, 1100), 1, 2000)
-    for B in (wide, long_row):
+    for B, tiled in ((wide, True), (long_row, False)):
         XB = np.random.default_rng(65).uniform(-1, 1, (B.numCols, 1))
         plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(B, gpu), 1)
-        assert not plan.stats()["tiled"]
+        assert plan.stats()["tiled"] == tiled
         Y = torch.empty((B.numRows, 1), dtype=torch.float64, device=gpu)
         plan.run(torch.from_numpy(XB).to(gpu), Y)
         torch.cuda.synchronize()

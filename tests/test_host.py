@@ -441,3 +441,43 @@ def test_knn3d_irregular_surrogate():
     rp32, ci32 = np.ascontiguousarray(rp, np.int32), np.ascontiguousarray(ci, np.int32)
     call("smfv_plan_analyse_rows", 0, A.numRows, A.numCols, rp32.ctypes.data_as(ip), ci32.ctypes.data_as(ip), 0, out)
     assert out[2] >= 3.0 and out[3] == 0  # re-use, direct rows
+
+
+def _chunks(A, r0=0, r1=None, cap=0):
+    out = (ctypes.c_double * 6)()
+    ip = ctypes.POINTER(ctypes.c_int)
+    r1 = A.numRows if r1 is None else r1
+    _lib.call("smfv_spmv_chunks_analyse", r0, r1, A.numCols, A.rowPtr.ctypes.data_as(ip),
+              A.colIndices.ctypes.data_as(ip), cap, out)
+    return {"fits": bool(out[0]), "chunks": int(out[1]), "entries": int(out[2]), "most_rows": int(out[3]),
+            "fill": out[4], "wide": bool(out[5])}
+
+
+def test_spmv_chunk_layout():
+    """The K = 1 chunk layout (k_spmv_chunks), built and verified natively as a
+    K = 1 plan builds it: every non-zero placed once, chunks full to > 95 % on
+    the cop20k stand-ins, at most 256 rows per chunk (one lane per row), a
+    row block's layout covers only its non-zeros; 16-bit column offsets on
+    the stencil, 32-bit columns where a row spans more than 2^16 columns (the
+    Morton-numbered k-NN stand-in); rows longer than a chunk leave the
+    pattern on the CSR kernel."""
+    for A, wide in ((smfv.cop20k_surrogate(), False), (smfv.inputs.cop20k_irregular_surrogate(), True)):
+        for cap in (1024, 2048):
+            c = _chunks(A, cap=cap)
+            assert c["fits"] and c["entries"] == A.nnz and c["fill"] > 0.95, (cap, c)
+            assert c["chunks"] >= A.nnz // cap and c["most_rows"] <= 256 and c["wide"] == wide
+    A = smfv.cop20k_surrogate()
+    c = _chunks(A, 1000, 50000)
+    assert c["fits"] and c["entries"] == int(A.rowPtr[50000] - A.rowPtr[1000])
+    # short rows: the 256-row cap ends chunks, not the entries
+    S = smfv.gen_random_rows(20000, 20000, 2.0, 0.0, 2, 5)
+    c = _chunks(S)
+    assert c["fits"] and c["most_rows"] == 256 and c["chunks"] == -(-20000 // 256) and not c["wide"]
+    # empty blocks and empty matrices
+    assert _chunks(A, 7, 7)["chunks"] == 0
+    E = smfv.readMatrixMarketFile(os.path.join(GOLDEN, "empty7x5.mtx"))
+    assert _chunks(E)["fits"]
+    # random columns over 10M: the wide layout; a row of 4,096 (> 2,048 slots): no chunk plan
+    assert _chunks(smfv.gen_random_rows(2000, 10_000_000, 16.0, 0.0, 16, 7))["wide"]
+    P = smfv.gen_random_rows(20000, 20000, 16, 2.0, 4096, 42)
+    assert np.diff(P.rowPtr).max() > 2048 and not _chunks(P, cap=2048)["fits"]
