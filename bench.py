@@ -77,6 +77,7 @@ CONFIGS = {
     # a second cop20k_A stand-in with the same m and nnz, unstructured (k-NN of
     # clustered 3-D points, row degrees 4..85): the plan on an irregular pattern
     "cop20kirr_k32": ("cop20k_irr", 32, "ROWWISE"),
+    "cop20kirr_k1": ("cop20k_irr", 1, "SEQUENTIAL"),
     # config 5: 80M x 80M, 16 nnz/row, row-partitioned over the ranks + RCCL all-gather
     "syn80m_k32": ("syn80m", 32, "ROWWISE"),
 }
