@@ -208,7 +208,7 @@ SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_
 SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int *h_row_ptr,
                                     const int *h_col_idx, int flags, double out[9]);
 /* The K = 1 chunk layout (k_spmv_chunks) of the row block [row_begin,
- * row_end) with `cap` entry slots per chunk (1024 or 2048; 0: the plans'
+ * row_end) with `cap` entry slots per chunk (512, 1024 or 2048; 0: the plans'
  * default), built and verified as smfv_plan_create builds it for K = 1:
  * out[0] 1 if the pattern fits the layout (else 0: a row longer than a
  * chunk), [1] chunks, [2] non-zeros placed, [3] most rows in a chunk, [4]

@@ -272,11 +272,14 @@ __global__ __launch_bounds__(NT) void k_spmv_stream(int row_begin, int nrows, co
 typedef double chunk_d2 __attribute__((ext_vector_type(2)));
 constexpr int K1_NT = 256;  // lanes per chunk block = row cap of a chunk
 
-// entry slots per chunk (1,024 or 2,048; lab builds: SMFV_K1_CHUNK)
+// entry slots per chunk (1,024; lab builds: SMFV_K1_CHUNK = 512 / 1,024 / 2,048)
 static int spmv_chunk_cap()
 {
 #ifdef SMFV_LAB
-    if (const char *e = std::getenv("SMFV_K1_CHUNK")) return std::atoi(e) == 2048 ? 2048 : 1024;
+    if (const char *e = std::getenv("SMFV_K1_CHUNK")) {
+        const int v = std::atoi(e);
+        return v == 2048 || v == 512 ? v : 1024;
+    }
 #endif
     return 1024;
 }
@@ -1945,7 +1948,7 @@ SMFV_API int smfv_spmv_chunks_analyse(int row_begin, int row_end, int n, const i
     SMFV_REQUIRE(row_begin >= 0 && row_end >= row_begin && n >= 0 && h_row_ptr_all && out &&
                      (h_row_ptr_all[row_end] == h_row_ptr_all[row_begin] || h_col_idx_all),
                  "bad argument");
-    SMFV_REQUIRE(cap == 0 || cap == 1024 || cap == 2048, "chunk cap must be 1024 or 2048");
+    SMFV_REQUIRE(cap == 0 || cap == 512 || cap == 1024 || cap == 2048, "chunk cap must be 512, 1024 or 2048");
     const int m = row_end - row_begin, base = h_row_ptr_all[row_begin];
     std::vector<int> rpl((size_t)m + 1);
     for (int i = 0; i <= m; ++i) rpl[i] = h_row_ptr_all[row_begin + i] - base;
@@ -2061,10 +2064,13 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     }
     if (plan->k1) {
         if (plan->ntiles > 0) {
-            auto kern = plan->k1_wide ? (plan->k1_cap == 2048 ? k_spmv_chunks<K1_NT, 2048, true>
-                                                              : k_spmv_chunks<K1_NT, 1024, true>)
-                                      : (plan->k1_cap == 2048 ? k_spmv_chunks<K1_NT, 2048, false>
-                                                              : k_spmv_chunks<K1_NT, 1024, false>);
+            auto kern = plan->k1_wide ? k_spmv_chunks<K1_NT, 1024, true> : k_spmv_chunks<K1_NT, 1024, false>;
+#ifdef SMFV_LAB
+            if (plan->k1_cap == 2048)
+                kern = plan->k1_wide ? k_spmv_chunks<K1_NT, 2048, true> : k_spmv_chunks<K1_NT, 2048, false>;
+            if (plan->k1_cap == 512)
+                kern = plan->k1_wide ? k_spmv_chunks<K1_NT, 512, true> : k_spmv_chunks<K1_NT, 512, false>;
+#endif
             hipLaunchKernelGGL(kern, dim3((unsigned)plan->ntiles), dim3(K1_NT), 0, st,
                                reinterpret_cast<const int4 *>(plan->k1_hdr), plan->k1_rs, plan->k1_off, plan->k1_col,
                                plan->tvals, d_X, ldx, d_Y, ldy);
