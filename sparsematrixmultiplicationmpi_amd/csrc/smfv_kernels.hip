@@ -323,8 +323,10 @@ __global__ __launch_bounds__(NT) void k_spmv_chunks(const int4 *__restrict__ hdr
     for (int k = 0; k < V2; ++k) {
         const int64_t j0 = WIDE ? (int64_t)(int)(uint32_t)cc[k] : (int64_t)(o[k] & 0xFFFFu);
         const int64_t j1 = WIDE ? (int64_t)(int)(uint32_t)(cc[k] >> 32) : (int64_t)(o[k] >> 16);
-        const double x0 = xb[j0 * ldx];
-        const double x1 = xb[j1 * ldx];
+        // pad slots gather nothing (a chunk of empty rows may sit on an empty X)
+        const int e0 = 2 * (k * NT + t);
+        const double x0 = e0 < h.w ? xb[j0 * ldx] : 0.0;
+        const double x1 = e0 + 1 < h.w ? xb[j1 * ldx] : 0.0;
         chunk_d2 p;
         p.x = v[k].x * x0;
         p.y = v[k].y * x1;

@@ -131,6 +131,11 @@ def test_degenerate_sizes(gpu):
     A = mat([0, 0, 0, 0], [], [], 3, 4)
     for v in smfv.Variant:
         assert np.all(run(v, A, np.ones((4, 3)), gpu) == 0.0)
+    # no columns at all (n = 0, X has no rows) at K = 1 and 32: Y is zeros
+    A = mat([0, 0, 0], [], [], 2, 0)
+    for K in (1, 32):
+        for v in smfv.Variant:
+            assert np.all(run(v, A, np.ones((0, K)), gpu) == 0.0), (v, K)
     # K = 0
     A = smfv.gen_fem27(100, 5, 5, 0.8, 1)
     for v in smfv.Variant:
