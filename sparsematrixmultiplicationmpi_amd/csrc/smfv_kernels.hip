@@ -1692,7 +1692,8 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
     // nnz-balanced merge path
     const bool whole_rows = variant != SMFV_NONZERO ||
                             (h_rp && h_rp[row_begin] == nnz_base && h_rp[row_begin + m] == nnz_end);
-    if (!rc && whole_rows && h_rp && h_ci && m > 0 && K > 0 && K % TILE_KP == 0 && !(flags & SMFV_PLAN_NO_TILES)) {
+    if (!rc && whole_rows && h_rp && h_ci && m > 0 && p->nnz > 0 && K > 0 && K % TILE_KP == 0 &&
+        !(flags & SMFV_PLAN_NO_TILES)) {  // (no non-zeros: nothing to stage)
         std::vector<int> rpl((size_t)m + 1);
         for (int i = 0; i <= m; ++i) rpl[i] = (int)(h_rp[row_begin + i] - nnz_base);
         const int *cil = h_ci + nnz_base;
