@@ -11,16 +11,33 @@
 static double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { std::printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 
-int main()
+int main(int argc, char **argv)
 {
+    const bool thp_first = argc > 1;  // trial order: huge pages first
     const size_t n = 64ull << 20;
     void *d = nullptr;
     CK(hipMalloc(&d, n));
     hipStream_t st;
     CK(hipStreamCreate(&st));
+    {
+        // the process's first copies: a 4 KiB pageable H2D and D2H (what a
+        // device start-up can absorb), then the 64 MB trials below
+        static char small[4096];
+        for (int k = 0; k < 2; ++k) {
+            double a = now();
+            CK(hipMemcpyAsync(d, small, sizeof small, hipMemcpyHostToDevice, st));
+            CK(hipStreamSynchronize(st));
+            double b = now();
+            CK(hipMemcpyAsync(small, d, sizeof small, hipMemcpyDeviceToHost, st));
+            CK(hipStreamSynchronize(st));
+            double c = now();
+            std::printf("{\"small_copy\": %d, \"h2d_ms\": %.3f, \"d2h_ms\": %.3f}\n", k, 1e3 * (b - a), 1e3 * (c - b));
+        }
+    }
     const char *names[3] = {"pageable_4k", "pageable_thp", "registered_thp"};
     for (int trial = 0; trial < 2; ++trial)
-        for (int mode = 0; mode < 3; ++mode) {
+        for (int mi = 0; mi < 3; ++mi) {
+            const int mode = thp_first ? (mi + 1) % 3 : mi;
             double t0 = now();
             char *h = (char *)mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
             if (h == MAP_FAILED) return 1;

@@ -134,6 +134,7 @@ struct Cached {
     void *p = nullptr;
     size_t cap = 0;
     bool host = false;
+    bool pinned = false;  // host: registered with HIP (hipHostRegister)
     void *get(size_t bytes)
     {
         if (bytes <= cap) return p;
@@ -145,6 +146,13 @@ struct Cached {
             if (q == MAP_FAILED) fail("mmap of host staging failed");
             (void)madvise(q, len, MADV_HUGEPAGE);
             par_touch(q, len);
+            // registered once, when allocated (0.1-1 ms for 64 MB of huge
+            // pages): copies from it run at ~57 GB/s from the first one, where
+            // a pageable copy's first large transfer in the process pays a
+            // one-time ~8 ms runtime start (scripts/micro/h2d_reg_probe.cpp);
+            // if registration fails the buffer stays pageable
+            pinned = hipHostRegister(q, len, hipHostRegisterDefault) == hipSuccess;
+            if (!pinned) (void)hipGetLastError();
             p = q;
             cap = len;
         } else {
@@ -156,11 +164,16 @@ struct Cached {
     void release()
     {
         if (p) {
-            if (host) munmap(p, cap);
-            else (void)hipFree(p);
+            if (host) {
+                if (pinned) (void)hipHostUnregister(p);
+                munmap(p, cap);
+            } else {
+                (void)hipFree(p);
+            }
         }
         p = nullptr;
         cap = 0;
+        pinned = false;
     }
     // fault the pages in now, in parallel (first touch)
     static void par_touch(void *q, size_t len);
@@ -168,9 +181,9 @@ struct Cached {
 
 struct Buffers {
     Cached rp, ci, va, X, Y, ref, hX{nullptr, 0, true}, hY{nullptr, 0, true};
-    // A's arrays staged into huge-page host memory before their upload: a
-    // caller's std::vector sits in 4 KiB pages, which HIP's pageable copy
-    // pins page by page (~6 GB/s measured) -- from huge pages it runs at ~50
+    // A's arrays staged into registered huge-page host memory before their
+    // upload (a caller's std::vector is pageable: its copies ran at ~6 GB/s on
+    // a first call, ~45 after, against ~57 from registered memory)
     Cached hrp{nullptr, 0, true}, hci{nullptr, 0, true}, hva{nullptr, 0, true};
     // the result of the last call on this rank (device) and the kept reference
     const double *lastY = nullptr;
