@@ -73,10 +73,12 @@ typedef enum smfv_status {
 /* ---- library ------------------------------------------------------------ */
 SMFV_API const char *smfv_last_error(void);
 SMFV_API const char *smfv_version(void);
-/* Creates the HIP context on the current device and loads the library's
- * code object (one empty kernel launch on `stream`, synchronised): the
- * one-time device start-up a CPU caller never pays, done before a timed call
- * so that call's time is the SpMM's. */
+/* Creates the HIP context on the current device, loads the library's code
+ * object (one empty kernel launch on `stream`) and starts the runtime's
+ * host<->device copy path (one 1 MiB copy each way: the process's first
+ * copy of that size costs 10-30 ms once), synchronised: the one-time device
+ * start-up a CPU caller never pays, done before a timed call so that call's
+ * time is the SpMM's. */
 SMFV_API int smfv_device_init(void *stream);
 
 /* ---- partitions (pure host functions, no device needed) ----------------- */

@@ -21,12 +21,13 @@
 #include "MatrixDefinitions.h"
 
 //   smfvInitDevice         the one-time device start-up (HIP context, code
-//                          object load) a CPU caller never pays, done before
-//                          the first timed call
+//                          object load, copy-path start) a CPU caller never
+//                          pays, done before the first timed call
 //   smfvLastCallTiming     the stage times of the last call (SMFV_TIMING=1)
 
-// Creates the HIP context on this rank's GPU and loads the library's code
-// object.  Returns its wall time (seconds).  Optional: the first call does
+// Creates the HIP context on this rank's GPU, loads the library's code
+// object and starts the runtime's host<->device copy path (smfv_device_init).
+// Returns its wall time (seconds).  Optional: the first call does
 // it otherwise, inside its own time.
 double smfvInitDevice();
 

@@ -6,6 +6,7 @@
 #include <sys/mman.h>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 static double now() { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
@@ -13,7 +14,11 @@ static double now() { return std::chrono::duration<double>(std::chrono::steady_c
 
 int main(int argc, char **argv)
 {
-    const bool thp_first = argc > 1;  // trial order: huge pages first
+    // trial order: argv[1] 'p' 4 KiB pages first, 't' huge pages first, 'g' registered first
+    const int shift = argc > 1 ? (argv[1][0] == 't' ? 1 : argv[1][0] == 'g' ? 2 : 0) : 0;
+    // argv[2]: MiB of a first warm-up copy (argv[3] 'r': from registered memory)
+    const size_t warm = argc > 2 ? (size_t)std::atoi(argv[2]) << 20 : 0;
+    const bool warm_reg = argc > 3 && argv[3][0] == 'r';
     const size_t n = 64ull << 20;
     void *d = nullptr;
     CK(hipMalloc(&d, n));
@@ -34,10 +39,21 @@ int main(int argc, char **argv)
             std::printf("{\"small_copy\": %d, \"h2d_ms\": %.3f, \"d2h_ms\": %.3f}\n", k, 1e3 * (b - a), 1e3 * (c - b));
         }
     }
+    if (warm) {
+        char *w = (char *)mmap(nullptr, warm, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        std::memset(w, 1, warm);
+        if (warm_reg) CK(hipHostRegister(w, warm, hipHostRegisterDefault));
+        double a = now();
+        CK(hipMemcpyAsync(d, w, warm, hipMemcpyHostToDevice, st));
+        CK(hipStreamSynchronize(st));
+        std::printf("{\"warm_MiB\": %zu, \"registered\": %d, \"ms\": %.3f}\n", warm >> 20, (int)warm_reg, 1e3 * (now() - a));
+        if (warm_reg) CK(hipHostUnregister(w));
+        munmap(w, warm);
+    }
     const char *names[3] = {"pageable_4k", "pageable_thp", "registered_thp"};
     for (int trial = 0; trial < 2; ++trial)
         for (int mi = 0; mi < 3; ++mi) {
-            const int mode = thp_first ? (mi + 1) % 3 : mi;
+            const int mode = (mi + shift) % 3;
             double t0 = now();
             char *h = (char *)mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
             if (h == MAP_FAILED) return 1;

@@ -1457,6 +1457,19 @@ SMFV_API int smfv_device_init(void *stream)
     hipStream_t st = as_stream(stream);
     hipLaunchKernelGGL(k_noop, dim3(1), dim3(64), 0, st);
     SMFV_LAUNCHED();
+    // the runtime starts its host<->device copy path on the first transfer of
+    // >= 1 MiB in the process (10-30 ms, whatever the memory; 4 KiB copies do
+    // not start it: scripts/micro/h2d_reg_probe.cpp) -- one 1 MiB copy each
+    // way here keeps that out of the first SpMM's H2D / D2H
+    constexpr size_t warm = (size_t)1 << 20;
+    std::vector<char> h(warm, 0);
+    void *d = nullptr;
+    SMFV_HIP(hipMalloc(&d, warm));
+    hipError_t e = hipMemcpyAsync(d, h.data(), warm, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(h.data(), d, warm, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(d);
+    SMFV_HIP(e);
     SMFV_HIP(hipStreamSynchronize(st));
     return SMFV_OK;
 }
