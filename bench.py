@@ -103,6 +103,8 @@ def kernel_label(variant: str, K: int, plan_stats: dict, x_bytes: int = 0) -> st
         return "k_merge_flat + k_carry_fixup" if K % 32 == 0 else "k_merge + k_carry_fixup"
     if plan_stats.get("mfma"):
         return "k_rows_mfma"
+    if plan_stats.get("kernel"):
+        return plan_stats["kernel"]
     if plan_stats.get("tiled"):
         return "k_spmv_chunks" if K == 1 else "k_rows_ws"
     if K == 1:
@@ -778,6 +780,9 @@ def main() -> None:
                     help="report the post-timing result check but do not fail on it (lab ablations)")
     ap.add_argument("--mfma", action="store_true",
                     help="time the opt-in dense-block MFMA tile kernel (SMFV_PLAN_MFMA, config 3's MFMA K-panel)")
+    ap.add_argument("--tiled-kernel", default="auto", choices=["auto", "cs", "ws"],
+                    help="tiled kernel for K % 32 == 0: the library's choice, k_rows_cs (SMFV_PLAN_CS) "
+                         "or k_rows_ws (SMFV_PLAN_WS), A/B")
     ap.add_argument("--fma", action="store_true",
                     help="time the opt-in FMA plans (SMFV_PLAN_FMA) instead of the bit-exact ones")
     ap.add_argument("--phase-timeout", type=float, default=240.0,
@@ -847,7 +852,8 @@ def main() -> None:
         torch.cuda.synchronize()
         t0 = time.time()
         plan = smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles, fma=args.fma, seeds=args.seeds,
-                             mfma=args.mfma, split_ends=args.split_ends, xcd_parts=args.xcd_parts)
+                             mfma=args.mfma, split_ends=args.split_ends, xcd_parts=args.xcd_parts,
+                             tiled_kernel=args.tiled_kernel)
         torch.cuda.synchronize()
         t_plan.append(time.time() - t0)
         copies.append((plan, dX, dY))

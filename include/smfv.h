@@ -179,6 +179,15 @@ typedef struct smfv_plan_s *smfv_plan_t;
  * variants are checked against (SC/main.cpp:184) -- so that check does not
  * compare a kernel with itself.  Ignored for SMFV_NONZERO. */
 #define SMFV_PLAN_SIMPLE_ROWS 128
+/* Column-streamed tiles (k_rows_cs, K % 32 == 0): two tiles of ~m / 512 rows
+ * per CU, each row's 32 panel columns held in registers for the whole tile,
+ * the tile's X rows streamed through LDS in column-sorted chunks; each row is
+ * still summed in CSR order (bit-identical).  Needs column-sorted CSR rows
+ * (otherwise the plan keeps k_rows_ws). */
+#define SMFV_PLAN_CS 256
+/* The former tiled kernel (k_rows_ws: ~60-row tiles whose whole X union sits
+ * in LDS) where SMFV_PLAN_CS would be the default (A/B). */
+#define SMFV_PLAN_WS 512
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
 /* Plan of the row block [row_begin, row_end) of a CSR matrix (h_row_ptr /
@@ -217,6 +226,15 @@ SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int
  * mean fill of a chunk's slots, [5] 1 for the wide layout (32-bit columns:
  * some row spans more than 65,535 columns), 0 for 16-bit offsets.  No device
  * needed.  (SC/SparseMatrixFatVectorMultiply.cpp:17-27 at vecCols = 1.) */
+/* The column-streamed tile plan (k_rows_cs, SMFV_PLAN_CS) of the row block
+ * [row_begin, row_end), built and verified as smfv_plan_create_rows builds it
+ * (rows_per_tile 0: the plan's own choice, else 1..256): out[0] tiles,
+ * [1] chunks, [2] staged X rows per panel, [3] re-use, [4] value slots incl.
+ * pads, [5] non-zeros, [6] chunks of the busiest block of the 8 x 32 grid,
+ * [7] steps of the busiest SIMD summed over the busiest block's chunks.
+ * No device needed. */
+SMFV_API int smfv_cs_plan_analyse(int row_begin, int row_end, int n, const int *h_row_ptr,
+                                  const int *h_col_idx, int flags, int rows_per_tile, double out[8]);
 SMFV_API int smfv_spmv_chunks_analyse(int row_begin, int row_end, int n, const int *h_row_ptr,
                                       const int *h_col_idx, int cap, double out[6]);
 SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int *d_col_idx,
@@ -229,8 +247,10 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
  * by each bind (snapshot entries, pads included), [10] 1 if the tiles run on
  * the MFMA kernel (SMFV_PLAN_MFMA), [11] XCD parts (8: one part of the
  * rows per XCD, 1: one wavefront), [12] X rows the 8 parts read, summed,
- * over the pattern's X rows (-1: not computed) */
-#define SMFV_PLAN_STATS 13
+ * over the pattern's X rows (-1: not computed), [13] the kernel a tiled
+ * plan runs: 0 none (untiled), 1 k_rows_ws, 2 k_rows_mfma, 3 k_spmv_chunks,
+ * 4 k_rows_cs; [14] chunks of a k_rows_cs plan */
+#define SMFV_PLAN_STATS 15
 SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS]);
 SMFV_API int smfv_plan_destroy(smfv_plan_t plan);
 

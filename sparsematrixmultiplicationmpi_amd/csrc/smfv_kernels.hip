@@ -805,6 +805,244 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
 #include "lab/ws_lab.inc"  // the instrumented lab copy (libsmfv_lab.so only)
 #endif
 
+// ---------------------------------------------------------------------------
+// k_rows_cs: column-streamed tiles (K % 32 == 0; plan build_cs_plan).
+// One persistent 1024-lane block per CU (grid 8 x CS_BLOCKS_PER_XCD), two
+// tiles of ~m / 512 rows per block.  Compute waves 0-7 hold 32 rows each, two
+// lanes per row, 16 panel columns per lane in registers (8 x d2) for the
+// whole tile; the tile's X rows, sorted by column, stream through LDS in
+// chunks of <= CS_XCAP rows, double-buffered: loader waves 8-15 stage chunk
+// u + 1 (its X rows, then its values and u8 offsets) by LDS-DMA while the
+// compute waves run chunk u.  Per step every row of a wave takes one entry:
+// a 16-byte value read per two steps, a 4-byte offset read per four, and 8
+// b128 X reads; a lane reads its 8 X pieces rotated by its row slot (piece
+// (k + p) & 7 into accumulator k), so the 16 lanes of a b128 lane group hit
+// 16 different bank quads whatever X rows they read: no bank conflicts.
+// A row's entries of chunk c are a contiguous run of its column-sorted CSR
+// row, and chunks ascend by column, so each row is summed in CSR order
+// (separate multiply and add; pads: -0.0 on the zero image row): bit-
+// identical to the reference loop.  A row's Y is stored right after the
+// chunk holding its last entry (the plan's tlast), spreading the stores over
+// the tile.  One barrier per chunk.
+// ---------------------------------------------------------------------------
+namespace cs {
+constexpr int XSLOT = (CS_XCAP + 1) * 256;  // X image: chunk rows + the zero row
+constexpr int SL_M = 2 * XSLOT;             // meta slots (values, then aux) follow the X slots
+constexpr int MSLOT = CS_MV + CS_MA;
+constexpr int ZOFF = CS_XCAP * 256;
+static_assert(SL_M + 2 * MSLOT <= 160 * 1024, "two X and two meta slots must fit the CU's 160 KiB");
+static_assert(XSLOT % 1024 == 0 && MSLOT % 1024 == 0 && CS_MV % 1024 == 0, "1 KiB DMA pieces");
+static_assert((CS_XCAP + 3) / 4 <= 64, "8 X pieces per loader wave cover a chunk");
+}  // namespace cs
+
+struct CsXcd {
+    int first[9];  // XCD x runs tiles [first[x], first[x + 1]); block j of it runs tiles first + j, + 32, ...
+};
+template <bool FMA = false>
+__global__ __launch_bounds__(1024, 1) void k_rows_cs(CsXcd xr, int npanel, const int2 *__restrict__ bs,
+                                                     const int *__restrict__ trow, const int *__restrict__ tlast,
+                                                     const int *__restrict__ crec, const uint8_t *__restrict__ aux,
+                                                     const double *__restrict__ tv, const double *__restrict__ X,
+                                                     int64_t ldx, double *__restrict__ Y, int64_t ldy)
+{
+    using namespace ws;
+    using cs::XSLOT;
+    using cs::SL_M;
+    using cs::MSLOT;
+    __shared__ __attribute__((aligned(16))) char lds[SL_M + 2 * MSLOT];
+    const int nb = gridDim.x >> 3, x = blockIdx.x & 7;
+    const int t0 = xr.first[x] + (blockIdx.x >> 3), tend = xr.first[x + 1];
+    const int2 b = bs[blockIdx.x];  // the block's first chunk, its chunks per panel
+    const int nunits = b.y * npanel;
+    if (t0 >= tend || nunits == 0) return;  // block-uniform
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const unsigned lds0 = (unsigned)(uintptr_t)lds;
+    if (wv >= 8) {
+        // ---------------- loader waves ----------------
+        __builtin_amdgcn_s_setprio(3);
+        const int wl = wv - 8;
+        if (wl == 0 && lane < 32)  // zero row of both X slots
+            reinterpret_cast<d2 *>(lds + (lane >> 4) * XSLOT + cs::ZOFF)[lane & 15] = d2{0.0, 0.0};
+        i4 u0, u1, f0, f1;  // the chunk record: X-row ids of this lane's pieces, fields
+        const unsigned ldxb = (unsigned)(ldx * 8);
+        auto fetch_record = [&](int cid) {
+            const int *G = crec + (int64_t)cid * CS_CWORDS;
+            const i4 *gu = reinterpret_cast<const i4 *>(G + 32 * wl + 8 * (lane >> 4));
+            u0 = gu[0];
+            u1 = gu[1];
+            const i4 *gf = reinterpret_cast<const i4 *>(G + 256 + 8 * (lane & 15));
+            f0 = gf[0];  // nx, vb, nvp, ab
+            f1 = gf[1];  // nap, c, nch, next
+        };
+        // stage the record's chunk, panel p, into slot s
+        auto stage = [&](int p, int s) {
+            asm volatile("" ::"v"(u0), "v"(u1), "v"(f0), "v"(f1));
+            const int nx = f0.x, nvp = f0.z, nap = f1.x;
+            const unsigned xb = lds0 + s * XSLOT;
+            const int uc[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int piece = wl + 8 * i;  // 1 KiB = chunk rows 4 piece .. + 3
+                const int u = 4 * piece + (lane >> 4);
+                if (4 * piece < nx && u < nx)
+                    dma16s<false>(X + p * TILE_KP, (unsigned)uc[i] * ldxb + 16u * (unsigned)(lane & 15),
+                                  xb + piece * 1024);
+            }
+            const unsigned mb = lds0 + SL_M + s * MSLOT;
+            const double *tvb = tv + __builtin_amdgcn_readfirstlane(f0.y);
+            const uint8_t *ab = aux + __builtin_amdgcn_readfirstlane(f0.w);
+            for (int k = wl; k < nvp; k += 8) dma16s<true>(tvb, 1024u * k + 16u * lane, mb + k * 1024);
+            for (int k = wl; k < nap; k += 8) dma16s<true>(ab, 1024u * k + 16u * lane, mb + CS_MV + k * 1024);
+        };
+        // unit after the record's one: the next chunk of the tile, the
+        // tile's next panel, or the block's next tile
+        auto advance = [&](int &cid, int &p) {
+            const int c = f1.y, nch = f1.z, next = f1.w;
+            if (c + 1 < nch) {
+                ++cid;
+            } else if (p + 1 < npanel) {
+                cid -= c;
+                ++p;
+            } else {
+                cid = next;
+                p = 0;
+            }
+        };
+        int cid = b.x, p = 0;
+        fetch_record(cid);
+        stage(0, 0);
+        advance(cid, p);
+        if (nunits > 1) fetch_record(cid);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_lds();
+        for (int u = 0; u < nunits; ++u) {
+            if (u + 1 < nunits) {
+                stage(p, (u + 1) & 1);
+                advance(cid, p);
+                if (u + 2 < nunits) fetch_record(cid);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // unit u + 1 has landed
+            barrier_lds();
+        }
+        return;
+    }
+    // ---------------- compute waves ----------------
+    auto madd = [](d2 a, double v, d2 x) -> d2 {
+        if constexpr (FMA)
+            return d2{__builtin_fma(v, x.x, a.x), __builtin_fma(v, x.y, a.y)};
+        else
+            return a + v * x;
+    };
+    const int rp_ = lane >> 1, h = lane & 1, slot = wv * CS_RPW + rp_;
+    // accumulator k <-> this lane's X piece (k + p) & 7 of its half row: byte
+    // offset h * 128 + ((rot + 16 k) & 112) (two VALU per read, no registers)
+    const unsigned rot = (unsigned)((rp_ & 7) * 16), hoff = (unsigned)(h * 128);
+    int t = t0;
+    int rowc = trow[(int64_t)t * CS_ROWS + slot], lastc = tlast[(int64_t)t * CS_ROWS + slot];
+    int rown = -1, lastn = 0;
+    if (t + nb < tend) {
+        rown = trow[(int64_t)(t + nb) * CS_ROWS + slot];
+        lastn = tlast[(int64_t)(t + nb) * CS_ROWS + slot];
+    }
+    d2 acc[8];
+    barrier_lds();
+    int p = 0;
+    for (int u = 0; u < nunits; ++u) {
+        const char *xbase = lds + (u & 1) * XSLOT;
+        const char *mbase = lds + SL_M + (u & 1) * MSLOT;
+        const int *H = reinterpret_cast<const int *>(mbase + CS_MV);
+        const int S = __builtin_amdgcn_readfirstlane(H[4 * wv]);
+        const int vo = __builtin_amdgcn_readfirstlane(H[4 * wv + 1]);
+        const int lo = __builtin_amdgcn_readfirstlane(H[4 * wv + 2]);
+        const int c = __builtin_amdgcn_readfirstlane(H[CS_H_C]);
+        const int nch = __builtin_amdgcn_readfirstlane(H[CS_H_NCH]);
+        if (c == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] = d2{0.0, 0.0};
+        }
+        const d2 *V = reinterpret_cast<const d2 *>(mbase) + vo / 2 + rp_;  // [s / 2][row] pairs
+        // software pipeline by half steps (4 of a step's 8 X pieces): the
+        // reads of the next half go out before the FP64 of this one (two
+        // ping-pong sets of 4 x d2); the values and offsets of a step pair
+        // are read a pair ahead (S is even).  Reads past the wave's last step
+        // (stale offsets) stay inside the block's LDS and are never summed.
+        const unsigned short *L = reinterpret_cast<const unsigned short *>(mbase + CS_MV + lo) + rp_;  // [s / 2][row]
+        auto load_h = [&](d2 *xv, unsigned o, int half) {
+            const char *xr_ = xbase + o * 256 + hoff;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                xv[k] = *reinterpret_cast<const d2 *>(xr_ + ((rot + 16u * (4 * half + k)) & 112u));
+        };
+        // one term = multiply then add (the reference's rounding), kept as
+        // one asm unit so the scheduler cannot hoist the multiplies ahead of
+        // their adds (more live registers)
+        auto fma4 = [&](double v, const d2 *xv, int half) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                d2 &a = acc[4 * half + k];
+                if constexpr (FMA) {
+                    a = madd(a, v, xv[k]);
+                } else {
+                    double t0, t1;
+                    asm("v_mul_f64 %0, %4, %5\n\tv_mul_f64 %1, %4, %6\n\t"
+                        "v_add_f64 %2, %2, %0\n\tv_add_f64 %3, %3, %1"
+                        : "=&v"(t0), "=&v"(t1), "+v"(a.x), "+v"(a.y)
+                        : "v"(v), "v"(xv[k].x), "v"(xv[k].y));
+                }
+            }
+        };
+        if (S > 0) {
+            d2 xa[4], xb[4];
+            d2 vP = V[0];
+            unsigned oP = L[0];
+            load_h(xa, oP & 0xFF, 0);
+            for (int i = 1;; ++i) {
+                load_h(xb, oP & 0xFF, 1);
+                __builtin_amdgcn_sched_barrier(0);
+                fma4(vP.x, xa, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                load_h(xa, oP >> 8, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                fma4(vP.x, xb, 1);
+                __builtin_amdgcn_sched_barrier(0);
+                const d2 vN = V[32 * i];
+                const unsigned oN = L[32 * i];
+                load_h(xb, oP >> 8, 1);
+                __builtin_amdgcn_sched_barrier(0);
+                fma4(vP.y, xa, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (2 * i >= S) {
+                    fma4(vP.y, xb, 1);
+                    break;
+                }
+                load_h(xa, oN & 0xFF, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                fma4(vP.y, xb, 1);
+                __builtin_amdgcn_sched_barrier(0);
+                vP = vN;
+                oP = oN;
+            }
+        }
+        if (rowc >= 0 && lastc == c) {
+            double *y = Y + (int64_t)rowc * ldy + p * TILE_KP + h * 16;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                __builtin_nontemporal_store(acc[k], reinterpret_cast<d2 *>(y + ((rot + 16u * k) & 112u) / 8));
+        }
+        if (c == nch - 1 && ++p == npanel) {
+            p = 0;
+            t += nb;
+            rowc = rown;
+            lastc = lastn;
+            if (t + nb < tend) {
+                rown = trow[(int64_t)(t + nb) * CS_ROWS + slot];
+                lastn = tlast[(int64_t)(t + nb) * CS_ROWS + slot];
+            }
+        }
+        barrier_lds();  // slot (u & 1) is free for unit u + 2
+    }
+}
+
 // Rows the ws plan could not tile (over a cap alone): one 8-lane team per
 // row, X gathered straight from HBM, CSR order (bit-identical).  `rows` are
 // block-local (Y row), row_begin + row indexes the CSR; the values come from
@@ -1632,6 +1870,12 @@ struct smfv_plan_s {
     uint16_t *k1_rs = nullptr, *k1_off = nullptr;
     int *k1_col = nullptr;                 // wide layout: 32-bit columns (k1_off unused)
     bool k1_wide = false;
+    bool cs = false;                       // k_rows_cs (column-streamed tiles), ntiles = tiles
+    int cs_chunks = 0;
+    int cs_xcd[9] = {};                    // XCD x runs tiles [cs_xcd[x], cs_xcd[x + 1])
+    int *cs_bs = nullptr;                  // per block of the 8 x 32 grid: first chunk, chunks per panel
+    int *cs_trow = nullptr, *cs_tlast = nullptr, *cs_crec = nullptr;
+    uint8_t *cs_aux = nullptr;
     void *ws = nullptr;
     size_t ws_bytes = 0, dev_bytes = 0;
     hipEvent_t bind_ev = nullptr;          // recorded after the snapshot gather
@@ -1640,7 +1884,8 @@ struct smfv_plan_s {
     {
         for (void *q : {(void *)tsrc, (void *)tvals, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
                         (void *)direct_off, (void *)ws_loff, ws, (void *)mf_rec, (void *)mf_ucols, (void *)mf_bstep,
-                        (void *)k1_hdr, (void *)k1_rs, (void *)k1_off, (void *)k1_col})
+                        (void *)k1_hdr, (void *)k1_rs, (void *)k1_off, (void *)k1_col, (void *)cs_bs,
+                        (void *)cs_trow, (void *)cs_tlast, (void *)cs_crec, (void *)cs_aux})
             if (q) (void)hipFree(q);
         if (bind_ev) (void)hipEventDestroy(bind_ev);
     }
@@ -1758,7 +2003,48 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                     p->dev_bytes += b;
                 }
             }
-        } else if (go) {
+        }
+        // column-streamed tiles (k_rows_cs) where asked for; a pattern the
+        // layout does not take (unsorted rows, ...) keeps k_rows_ws
+        if (!rc && go && !(flags & SMFV_PLAN_MFMA) && (flags & SMFV_PLAN_CS) && !(flags & SMFV_PLAN_WS)) {
+            CsPlan C;
+            std::string err;
+            if (build_cs_plan(m, n, rpl.data(), cil, C, &err, caps)) {
+                p->tiled = p->cs = true;
+                p->ntiles = C.ntiles;
+                p->cs_chunks = C.nchunks;
+                for (int x = 0; x <= 8; ++x) p->cs_xcd[x] = C.xcd[x];
+                p->parts = caps.part_start.size() > 2 ? (int)caps.part_start.size() - 1 : 1;
+                p->union_rows = C.union_rows;
+                p->tiled_nnz = C.tiled_nnz;
+                p->padded_nnz = C.entries;
+                p->reuse = C.union_rows ? (double)C.tiled_nnz / (double)C.union_rows : 0.0;
+                // per block of the 8 x 32 grid: its first chunk and its chunks (one panel)
+                std::vector<int> bs(2 * 8 * CS_BLOCKS_PER_XCD, 0);
+                for (int blk = 0; blk < 8 * CS_BLOCKS_PER_XCD; ++blk) {
+                    const int x = blk & 7, t0 = C.xcd[x] + (blk >> 3);
+                    if (t0 >= C.xcd[x + 1]) continue;
+                    bs[2 * blk] = C.tfirst[(size_t)t0];
+                    for (int t = t0; t < C.xcd[x + 1]; t += CS_BLOCKS_PER_XCD)
+                        bs[2 * blk + 1] += (t + 1 < C.ntiles ? C.tfirst[(size_t)t + 1] : C.nchunks) - C.tfirst[(size_t)t];
+                }
+                for (int &q : C.tsrc)
+                    if (q >= 0) q += (int)nnz_base;
+                p->snapshot = (int64_t)C.tsrc.size();
+                if (!rc) rc = upload(&p->cs_bs, bs, p->dev_bytes);
+                if (!rc) rc = upload(&p->cs_trow, C.trow, p->dev_bytes);
+                if (!rc) rc = upload(&p->cs_tlast, C.tlast, p->dev_bytes);
+                if (!rc) rc = upload(&p->cs_crec, C.crec, p->dev_bytes);
+                if (!rc) rc = upload(&p->cs_aux, C.aux, p->dev_bytes);
+                if (!rc) rc = upload(&p->tsrc, C.tsrc, p->dev_bytes);
+                if (!rc) {
+                    const size_t b = std::max<size_t>((size_t)p->snapshot, 1) * sizeof(double);
+                    fail_hip(hipMalloc(reinterpret_cast<void **>(&p->tvals), b), "hipMalloc(tvals)");
+                    p->dev_bytes += b;
+                }
+            }
+        }
+        if (!rc && go && !p->mfma && !p->cs && !(flags & SMFV_PLAN_MFMA)) {
             WsPlan W;
             std::string err;
             if (!build_ws_plan(m, n, rpl.data(), cil, W, &err, caps)) {
@@ -1958,6 +2244,49 @@ SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int
     return SMFV_OK;
 }
 
+SMFV_API int smfv_cs_plan_analyse(int row_begin, int row_end, int n, const int *h_row_ptr_all,
+                                  const int *h_col_idx_all, int flags, int rows_per_tile, double out[8])
+{
+    SMFV_REQUIRE(row_begin >= 0 && row_end >= row_begin && n >= 0 && h_row_ptr_all && out &&
+                     (h_row_ptr_all[row_end] == h_row_ptr_all[row_begin] || h_col_idx_all),
+                 "bad argument");
+    SMFV_REQUIRE(rows_per_tile >= 0 && rows_per_tile <= CS_ROWS, "rows per tile must be 0..%d", CS_ROWS);
+    const int m = row_end - row_begin, base = h_row_ptr_all[row_begin];
+    std::vector<int> rpl((size_t)m + 1);
+    for (int i = 0; i <= m; ++i) rpl[i] = h_row_ptr_all[row_begin + i] - base;
+    const int *cil = h_col_idx_all ? h_col_idx_all + base : nullptr;
+    TileCaps caps = plan_caps(flags, row_begin);
+    double footprint = -1.0;
+    plan_parts(caps, flags, m, n, rpl.data(), cil, &footprint);
+    caps.cs_rows = rows_per_tile;
+    CsPlan C;
+    std::string err;
+    if (!build_cs_plan(m, n, rpl.data(), cil, C, &err, caps)) {
+        set_error("%s", err.c_str());
+        return SMFV_ERR_INVALID;
+    }
+    int most = 0, steps = 0;  // chunks / SIMD steps of the busiest block of the 8 x 32 grid
+    for (int blk = 0; blk < 8 * CS_BLOCKS_PER_XCD; ++blk) {
+        const int x = blk & 7;
+        int units = 0, st = 0;
+        for (int t = C.xcd[x] + (blk >> 3); t < C.xcd[x + 1]; t += CS_BLOCKS_PER_XCD) {
+            units += (t + 1 < C.ntiles ? C.tfirst[(size_t)t + 1] : C.nchunks) - C.tfirst[(size_t)t];
+            st += C.tsimd[(size_t)t];
+        }
+        most = std::max(most, units);
+        steps = std::max(steps, st);
+    }
+    out[0] = C.ntiles;
+    out[1] = C.nchunks;
+    out[2] = (double)C.union_rows;
+    out[3] = C.union_rows ? (double)C.tiled_nnz / (double)C.union_rows : 0.0;
+    out[4] = (double)C.entries;
+    out[5] = (double)C.tiled_nnz;
+    out[6] = most;
+    out[7] = steps;
+    return SMFV_OK;
+}
+
 SMFV_API int smfv_spmv_chunks_analyse(int row_begin, int row_end, int n, const int *h_row_ptr_all,
                                       const int *h_col_idx_all, int cap, double out[6])
 {
@@ -2039,6 +2368,8 @@ SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS])
     out[10] = plan->mfma ? 1.0 : 0.0;
     out[11] = plan->parts;
     out[12] = plan->footprint;
+    out[13] = !plan->tiled ? 0.0 : plan->cs ? 4.0 : plan->k1 ? 3.0 : plan->mfma ? 2.0 : 1.0;
+    out[14] = plan->cs_chunks;
     return SMFV_OK;
 }
 
@@ -2098,6 +2429,22 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     if (hipGetDevice(&dev) == hipSuccess) {
         int v = 0;
         if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
+    }
+    if (plan->cs) {
+        // 8 x 32 persistent blocks (the plan's per-block chunk lists assume
+        // that grid; on a chip with fewer CUs blocks queue, still correct);
+        // the loaders address X, the snapshot and the aux bytes by scalar
+        // base + 32-bit offset
+        if ((uint64_t)plan->n * (uint64_t)ldx * 8u >= (1ull << 32))
+            return launch_rows(plan->row_begin, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, plan->n, K, d_Y, ldy,
+                               st);
+        CsXcd xr;
+        for (int x = 0; x <= 8; ++x) xr.first[x] = plan->cs_xcd[x];
+        hipLaunchKernelGGL(plan->fma ? k_rows_cs<true> : k_rows_cs<false>, dim3(8 * CS_BLOCKS_PER_XCD), dim3(1024),
+                           0, st, xr, K / TILE_KP, reinterpret_cast<const int2 *>(plan->cs_bs), plan->cs_trow,
+                           plan->cs_tlast, plan->cs_crec, plan->cs_aux, plan->tvals, d_X, ldx, d_Y, ldy);
+        SMFV_LAUNCHED();
+        return SMFV_OK;
     }
     if (plan->mfma) {
         if (plan->ntiles > 0) {

@@ -116,8 +116,9 @@ def _check_dense(T: torch.Tensor, rows: int, K: int, name: str) -> int:
 
 
 PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA, PLAN_NATURAL_SEEDS, PLAN_MFMA, PLAN_SPLIT_ENDS = 1, 2, 4, 8, 16, 32
-PLAN_ONE_WAVEFRONT = 64
-PLAN_STATS = 13  # SMFV_PLAN_STATS
+PLAN_ONE_WAVEFRONT, PLAN_SIMPLE_ROWS, PLAN_CS, PLAN_WS = 64, 128, 256, 512
+PLAN_STATS = 15  # SMFV_PLAN_STATS
+PLAN_KERNELS = {0: None, 1: "k_rows_ws", 2: "k_rows_mfma", 3: "k_spmv_chunks", 4: "k_rows_cs"}
 
 
 class SpmmPlan:
@@ -137,7 +138,7 @@ class SpmmPlan:
     def __init__(self, variant: int, A: DeviceCSR, K: int, tiles: str = "auto", fma: bool = False,
                  stream: torch.cuda.Stream | None = None, rows: tuple[int, int] | None = None,
                  seeds: str = "frontier", mfma: bool = False, split_ends: bool = False,
-                 xcd_parts: str = "auto"):
+                 xcd_parts: str = "auto", tiled_kernel: str = "auto"):
         self.variant, self.A, self.K = Variant(variant), A, K
         self.rows = rows
         flags = {"auto": 0, "off": PLAN_NO_TILES, "force": PLAN_FORCE_TILES}[tiles]
@@ -151,6 +152,9 @@ class SpmmPlan:
             flags |= PLAN_SPLIT_ENDS
         if {"auto": False, "one": True}[xcd_parts]:
             flags |= PLAN_ONE_WAVEFRONT
+        # which tiled kernel for K % 32 == 0: the library's choice, or k_rows_cs
+        # (column-streamed tiles, SMFV_PLAN_CS) / k_rows_ws (SMFV_PLAN_WS) for A/B
+        flags |= {"auto": 0, "cs": PLAN_CS, "ws": PLAN_WS}[tiled_kernel]
         self._plan = ctypes.c_void_p()
         ip = ctypes.POINTER(ctypes.c_int)
         if rows is None:
@@ -176,7 +180,7 @@ class SpmmPlan:
                 "reuse": float(out[3]), "plan_bytes": int(out[4]), "direct_rows": int(out[5]),
                 "row_begin": int(out[6]), "est_reuse": float(out[7]), "analysis_ms": float(out[8]),
                 "snapshot_entries": int(out[9]), "mfma": bool(out[10]), "xcd_parts": int(out[11]),
-                "footprint": float(out[12])}
+                "footprint": float(out[12]), "kernel": PLAN_KERNELS.get(int(out[13])), "chunks": int(out[14])}
 
     def run(self, X: torch.Tensor, Y: torch.Tensor, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
         A, K = self.A, self.K
