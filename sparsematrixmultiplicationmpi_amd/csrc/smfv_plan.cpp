@@ -840,16 +840,11 @@ bool cs_emit_tile(const std::vector<int> &rows_in, int t, const int *rp, const i
     const int nr = (int)rows.size(), per = (nr + CS_WAVES - 1) / CS_WAVES;
     for (int s = 0; s < CS_ROWS; ++s) T.slot_row[s] = -1, T.slot_last[s] = 0;
     std::vector<int> slots;  // slot of the k-th row
-    static const int deal = [] {
-        const char *e = std::getenv("SMFV_CS_DEAL");
-        return e ? std::atoi(e) : 0;
-    }();
+    // contiguous runs: wave w takes sorted rows [w per, (w + 1) per), so the
+    // waves sharing a SIMD (w, w + 4) hold rows far apart in column order
+    // (measured against round robin and adjacent pairs: fewest SIMD steps)
     for (int k = 0; k < nr; ++k) {
-        // 0: contiguous runs (wave w: sorted rows [w per, (w + 1) per)); 1: round robin;
-        // 2: contiguous runs, run i on wave (i even: i / 2, odd: 4 + i / 2) -- the
-        // waves sharing a SIMD (w, w + 4) hold runs far apart in column order
-        const int run = k / per, w = deal == 1 ? k % CS_WAVES : deal == 2 ? (run % 2 ? 4 + run / 2 : run / 2) : run;
-        const int s = w * CS_RPW + (deal == 1 ? k / CS_WAVES : k % per);
+        const int s = (k / per) * CS_RPW + k % per;
         T.slot_row[s] = rows[(size_t)k];
         slots.push_back(s);
     }
@@ -935,10 +930,7 @@ bool cs_emit_tile(const std::vector<int> &rows_in, int t, const int *rp, const i
     // [a, b) is feasible when its X rows and its (even-rounded) steps fit the
     // LDS slots; it costs the steps of its busiest SIMD (waves w and w + 4
     // share one) plus a per-chunk overhead; the cuts minimise the tile's sum
-    static const int lambda = [] {
-        const char *e = std::getenv("SMFV_CS_LAMBDA");
-        return e ? std::atoi(e) : 8;
-    }();
+    constexpr int lambda = 8;  // per-chunk overhead in steps (4 and 16: no better on the cop20k stand-ins)
     auto cost_of = [&](const int *Sw) {
         int most = 0;
         for (int q = 0; q < CS_WAVES / 2; ++q)
@@ -972,7 +964,6 @@ bool cs_emit_tile(const std::vector<int> &rows_in, int t, const int *rp, const i
     std::vector<int> cuts;
     for (int b = nu; b > 0; b = from[(size_t)b]) cuts.push_back(b);
     std::reverse(cuts.begin(), cuts.end());
-    static const bool dbg = std::getenv("SMFV_CS_DEBUG") != nullptr;
     int u0 = 0;
     for (size_t k = 0; k + 1 < cuts.size() || (k < cuts.size() && cuts[k] < nu); ++k) {
         const int u1 = cuts[k];
@@ -982,11 +973,6 @@ bool cs_emit_tile(const std::vector<int> &rows_in, int t, const int *rp, const i
             S[s / CS_RPW] = std::max(S[s / CS_RPW], ++cnt[s]);
         }
         for (int e = bstart[(size_t)u0]; e < bstart[(size_t)u1]; ++e) cnt[bslot[(size_t)e]] = 0;
-        if (dbg && t < 3) {
-            std::fprintf(stderr, "tile %d chunk %d: nx %d, steps", t, T.nch, u1 - u0);
-            for (int w = 0; w < CS_WAVES; ++w) std::fprintf(stderr, " %d", S[w]);
-            std::fprintf(stderr, "\n");
-        }
         emit_chunk(u0, u1);
         u0 = u1;
     }
@@ -996,13 +982,6 @@ bool cs_emit_tile(const std::vector<int> &rows_in, int t, const int *rp, const i
         S[s / CS_RPW] = std::max(S[s / CS_RPW], ++cnt[s]);
     }
     emit_chunk(u0, nu);  // (a tile without non-zeros gets one empty chunk: its rows store zeros)
-    if (dbg && t < 3) {
-        int ss = 0;
-        for (int w = 0; w < CS_WAVES; ++w) ss += S[w];
-        std::fprintf(stderr, "tile %d last chunk: steps", t);
-        for (int w = 0; w < CS_WAVES; ++w) std::fprintf(stderr, " %d", S[w]);
-        std::fprintf(stderr, " (sum %d)\n", ss);
-    }
     for (int c = 0; c < T.nch; ++c) {
         const int ab = T.rec[(size_t)c * CS_CWORDS + 256 + CS_C_AB];
         reinterpret_cast<int *>(&T.aux[(size_t)ab])[CS_H_NCH] = T.nch;
@@ -1049,14 +1028,21 @@ bool build_cs_plan(int m, int n, const int *rp, const int *ci, CsPlan &P, std::s
     caps.ucap = 1 << 30;
     caps.ncap = 1 << 30;
     caps.pad = 1;
-    TileAnalysis A;
-    analyse_tiles(m, n, rp, ci, A, caps);
-    tick("analyse_tiles");
-    const int nt = (int)A.meta.size();
-    const int np = (int)A.part_tile.size() - 1;
+    // tiles: the clustered row analysis at this tile size
+    std::vector<std::vector<int>> tl;
+    std::vector<int> part_tile;
+    {
+        TileAnalysis A;
+        analyse_tiles(m, n, rp, ci, A, caps);
+        for (const TileMeta &tm : A.meta) tl.emplace_back(A.grow.begin() + tm.roff, A.grow.begin() + tm.roff + tm.nrows);
+        part_tile = A.part_tile;
+    }
+    tick("tiles");
+    const int nt = (int)tl.size();
+    const int np = (int)part_tile.size() - 1;
     P.ntiles = nt;
     for (int x = 0; x <= 8; ++x)
-        P.xcd[x] = np == 8 ? A.part_tile[(size_t)x] : (int)((int64_t)nt * x / 8);
+        P.xcd[x] = np == 8 ? part_tile[(size_t)x] : (int)((int64_t)nt * x / 8);
     P.xcd[8] = nt;
     // tiles emitted in parallel, then concatenated in order
     std::vector<CsTile> out((size_t)nt);
@@ -1068,9 +1054,8 @@ bool build_cs_plan(int m, int n, const int *rp, const int *ci, CsPlan &P, std::s
         auto work = [&](int w) {
             std::vector<int> pos((size_t)std::max(n, 1), -1);
             for (int t = (int)((int64_t)nt * w / nth); t < (int)((int64_t)nt * (w + 1) / nth) && !bad[(size_t)w]; ++t) {
-                const TileMeta &tm = A.meta[(size_t)t];
-                std::vector<int> R(A.grow.begin() + tm.roff, A.grow.begin() + tm.roff + tm.nrows);
-                if (!cs_emit_tile(R, t, rp, ci, pos, out[(size_t)t], why[(size_t)t])) bad[(size_t)w] = 1;
+                if (!cs_emit_tile(tl[(size_t)t], t, rp, ci, pos, out[(size_t)t], why[(size_t)t]))
+                    bad[(size_t)w] = 1;
             }
         };
         std::vector<std::thread> pool;

@@ -481,3 +481,22 @@ def test_spmv_chunk_layout():
     assert _chunks(smfv.gen_random_rows(2000, 10_000_000, 16.0, 0.0, 16, 7))["wide"]
     P = smfv.gen_random_rows(20000, 20000, 16, 2.0, 4096, 42)
     assert np.diff(P.rowPtr).max() > 2048 and not _chunks(P, cap=2048)["fits"]
+
+
+def test_column_streamed_plan_layout():
+    """The opt-in column-streamed tile plan (k_rows_cs, SMFV_PLAN_CS), built and
+    verified natively (every row's entries replayed chunk by chunk in CSR
+    order, pads on the zero image row): on the cop20k stand-in about two tiles
+    per CU, several chunks per tile, more X re-use than the k_rows_ws tiles;
+    a row whose columns are not sorted is refused (the plan keeps k_rows_ws)."""
+    A = smfv.inputs.cop20k_surrogate()
+    ip = ctypes.POINTER(ctypes.c_int)
+    out = (ctypes.c_double * 8)()
+    _lib.call("smfv_cs_plan_analyse", 0, A.numRows, A.numCols, A.rowPtr.ctypes.data_as(ip),
+              A.colIndices.ctypes.data_as(ip), 0, 0, out)
+    tiles, chunks, reuse, nnz = int(out[0]), int(out[1]), out[3], int(out[5])
+    assert 256 < tiles <= 512 and chunks > 2 * tiles and reuse > 6.0 and nnz == A.nnz
+    rp = np.array([0, 3, 5], np.int32)
+    ci = np.array([0, 2, 1, 1, 0], np.int32)  # row 1 unsorted
+    with pytest.raises(RuntimeError, match="column-sorted"):
+        _lib.call("smfv_cs_plan_analyse", 0, 2, 3, rp.ctypes.data_as(ip), ci.ctypes.data_as(ip), 0, 0, out)
