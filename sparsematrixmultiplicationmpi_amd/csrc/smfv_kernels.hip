@@ -2478,7 +2478,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
                   : abl == 1 ? k_rows_ws_lab<1> : abl == 2 ? k_rows_ws_lab<2> : abl == 3 ? k_rows_ws_lab<3>
                   : abl == 4 ? k_rows_ws_lab<4> : abl == 5 ? k_rows_ws_lab<5> : abl == 6 ? k_rows_ws_lab<6>
                   : abl == 7 ? k_rows_ws_lab<7> : abl == 8 ? k_rows_ws_lab<8> : abl == 12 ? k_rows_ws_lab<12>
-                  : abl == 13 ? k_rows_ws_lab<13> : abl == 14 ? k_rows_ws_lab<14> : abl == 15 ? k_rows_ws_lab<15>
+                  : abl == 13 ? k_rows_ws_lab<13> : abl == 14 ? k_rows_ws_lab<14> : abl == 15 ? k_rows_ws_lab<15> : abl == 16 ? k_rows_ws_lab<16>
                   : abl == 9 ? (K == TILE_KP ? k_rows_ws_lab<9> : k_rows_ws<>)
                   : abl == 10 ? (K == TILE_KP ? k_rows_ws_lab<10> : k_rows_ws<>)
                   : abl == 11 ? (K == TILE_KP ? k_rows_ws_lab<11> : k_rows_ws<>) : k_rows_ws<>;
