@@ -489,11 +489,11 @@ __global__ __launch_bounds__(256) void k_rows_mh(int row_begin, int nrows,
 //  * waves 8-15 (loaders) stage the next work unit into the other half of a
 //    double-buffered LDS image by LDS-DMA (global_load_lds_dwordx4);
 //  * waves 0-7 (compute) run 64 eight-lane teams, one row each, out of LDS:
-//    per batch of 8 entries, one b128 read of 8 offsets, four of 8 values,
+//    per batch of 8 entries, one b64 read of 8 u8 image rows, four of 8 values,
 //    16 b128 X reads; the next batch's meta is read behind this batch's X.
 // A work unit is (tile, 32-column panel), panels innermost: a unit stages
 // the tile's union of X rows for its panel (<= 255 x 256 B; image row 255
-// stays zero) into X slot (unit & 1); the tile's values, u16 X-row offsets
+// stays zero) into X slot (unit & 1); the tile's values, u8 X-image rows
 // (tile-ordered, interleaved per quad of teams, build_ws_plan) and 1 KiB
 // record are staged once per tile, with its first panel, into meta slot
 // (tile & 1) -- K = 128 reads them once, not four times.
@@ -510,8 +510,8 @@ __global__ __launch_bounds__(256) void k_rows_mh(int row_begin, int nrows,
 namespace ws {
 constexpr int XSLOT = (WS_UCAP + 1) * 256;  // X image: union rows + the zero row, 256 B each
 constexpr int SL_M = 2 * XSLOT;             // meta slots follow the X slots
-// values and offsets arrive in whole 1 KiB DMA pieces (128 doubles / 512 u16)
-constexpr int M_V = 0, M_L = (WS_NCAP + 127) / 128 * 1024, M_R = M_L + (WS_NCAP + 511) / 512 * 1024,
+// values and offsets arrive in whole 1 KiB DMA pieces (128 doubles / 1,024 u8)
+constexpr int M_V = 0, M_L = (WS_NCAP + 127) / 128 * 1024, M_R = M_L + (WS_NCAP + 1023) / 1024 * 1024,
               MSLOT = M_R + WS_LWORDS * 4;
 static_assert(SL_M + 2 * MSLOT <= 160 * 1024, "two X and two meta slots must fit the CU's 160 KiB");
 static_assert(XSLOT % 1024 == 0 && MSLOT % 1024 == 0, "1 KiB DMA pieces");
@@ -519,6 +519,7 @@ static_assert(WS_UCAP + 1 <= 4 * 8 * WS_LOADERS, "8 X pieces per loader wave cov
 typedef double d2 __attribute__((ext_vector_type(2)));
 typedef int i4 __attribute__((ext_vector_type(4)));
 typedef unsigned u4 __attribute__((ext_vector_type(4)));
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
 
 // LDS-DMA of 16 B per lane to lds_dst + 16 * lane (M0 written in the same
 // statement, MI355X guide recipe); NT: non-temporal source read.
@@ -566,7 +567,7 @@ template <bool FMA = false, bool SADDR = true>
 __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int chunked,
                                                      const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
-                                                     const uint16_t *__restrict__ loff,
+                                                     const uint8_t *__restrict__ loff,
                                                      const double *__restrict__ tv,
                                                      const double *__restrict__ X, int64_t ldx,
                                                      double *__restrict__ Y, int64_t ldy)
@@ -609,7 +610,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
         if (wl == 0 && lane < 32)  // zero row of both X slots
             reinterpret_cast<d2 *>(lds + (lane >> 4) * XSLOT + WS_ZOFF)[lane & 15] = d2{0.0, 0.0};
         i4 u0, u1;
-        int noff, tn, nu;
+        int noff, tn, nu, voff, tnv;
         unsigned xo[8];                       // SADDR: byte offset of this lane's 16 B of union row uc[i]
         const unsigned ldxb = (unsigned)(ldx * 8);
         auto fetch_record = [&](int t) {
@@ -620,12 +621,14 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
             noff = G[WS_G_NOFF + (lane & 15)];
             tn = G[WS_G_TN + (lane & 15)];
             nu = G[WS_G_NU + (lane & 15)];
+            voff = G[WS_G_VOFF + (lane & 15)];
+            tnv = G[WS_G_TNV + (lane & 15)];
         };
         // stage unit (tile t, panel p): X rows into X slot xs, and (first panel) the meta into slot ms
         auto stage = [&](int t, int p, int xs, int ms) {
             // hipcc does not count the asm DMAs: resolve the record registers
             // here, so no wait it places for them lands between two DMAs
-            asm volatile("" ::"v"(u0), "v"(u1), "v"(noff), "v"(tn), "v"(nu));
+            asm volatile("" ::"v"(u0), "v"(u1), "v"(noff), "v"(tn), "v"(nu), "v"(voff), "v"(tnv));
             const unsigned xb = lds0 + xs * XSLOT;
             const int uc[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
             const int cp = p * TILE_KP;
@@ -637,18 +640,18 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
                 const unsigned mb = lds0 + SL_M + ms * MSLOT;
                 if constexpr (SADDR) {
                     const int nf = __builtin_amdgcn_readfirstlane(noff);
-                    const double *tvb = tv + nf;
-                    const uint16_t *lb = loff + nf;
-                    for (int k = wl; k * 128 < tn; k += WS_LOADERS)
+                    const double *tvb = tv + __builtin_amdgcn_readfirstlane(voff);
+                    const uint8_t *lb = loff + nf;
+                    for (int k = wl; k * 128 < tnv; k += WS_LOADERS)
                         dma16s<true>(tvb, 1024u * k + 16u * lane, mb + M_V + k * 1024);
-                    for (int k = wl; k * 512 < tn; k += WS_LOADERS)
+                    for (int k = wl; k * 1024 < tn; k += WS_LOADERS)
                         dma16s<true>(lb, 1024u * k + 16u * lane, mb + M_L + k * 1024);
                     if (wl == WS_LOADERS - 1) dma16s<true>(lrec + (int64_t)t * WS_LWORDS, 16u * lane, mb + M_R);
                 } else {
-                    for (int k = wl; k * 128 < tn; k += WS_LOADERS)
-                        dma16<true>(tv + noff + 128 * k + 2 * lane, mb + M_V + k * 1024);
-                    for (int k = wl; k * 512 < tn; k += WS_LOADERS)
-                        dma16<true>(loff + noff + 512 * k + 8 * lane, mb + M_L + k * 1024);
+                    for (int k = wl; k * 128 < tnv; k += WS_LOADERS)
+                        dma16<true>(tv + voff + 128 * k + 2 * lane, mb + M_V + k * 1024);
+                    for (int k = wl; k * 1024 < tn; k += WS_LOADERS)
+                        dma16<true>(loff + noff + 1024 * k + 16 * lane, mb + M_L + k * 1024);
                     if (wl == WS_LOADERS - 1) dma16<true>(lrec + (int64_t)t * WS_LWORDS + 4 * lane, mb + M_R);
                 }
             };
@@ -711,7 +714,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
             // entries of one more (its length rounded up to even)
             const int js = info & 0xFFFF, len = info >> 16, nbat = len >> 3, rem = len & 7;
             const int blast = nbat + (rem ? 1 : 0) - 1;
-            const u4 *Lq = reinterpret_cast<const u4 *>(mbase + M_L) + js + qk;
+            const u2 *Lq = reinterpret_cast<const u2 *>(mbase + M_L) + js + qk;
             const d2 *Vq = reinterpret_cast<const d2 *>(mbase + M_V) + R[128 + slot] + qk;
             const char *xb0 = xbase + par * 128 + tl * 16;
             const char *xb1 = xbase + (par ^ 1) * 128 + tl * 16;
@@ -720,27 +723,43 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
             // four; X is read in halves of 4 entries, ping-pong: the reads of
             // the next half go out before the current half is summed, so each
             // half's LDS latency hides behind the other half's FP64 work
-            auto rdx = [&](unsigned w, d2 &a0, d2 &a1, d2 &b0, d2 &b1) {
-                a0 = *reinterpret_cast<const d2 *>(xb0 + (w & 0xFFFF));
-                b0 = *reinterpret_cast<const d2 *>(xb0 + (w >> 16));
-                a1 = *reinterpret_cast<const d2 *>(xb1 + (w & 0xFFFF));
-                b1 = *reinterpret_cast<const d2 *>(xb1 + (w >> 16));
+            // two entries' X reads from a word of four u8 image rows: one
+            // v_perm_b32 spreads rows h, h+1 into the high bytes of two u16
+            // halves (row * 256 = the byte offset), the address adds take
+            // them as words (SDWA), as they did for u16 offsets
+            const unsigned xo0 = (unsigned)(xb0 - lds), xo1 = (unsigned)(xb1 - lds);
+            auto rdx = [&](unsigned w, unsigned sel, d2 &a0, d2 &a1, d2 &b0, d2 &b1) {
+                const unsigned pw = __builtin_amdgcn_perm(0u, w, sel);
+                unsigned r0, r1, r2, r3;
+                asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+                    : "=v"(r0) : "v"(xo0), "v"(pw));
+                asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+                    : "=v"(r1) : "v"(xo0), "v"(pw));
+                asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0"
+                    : "=v"(r2) : "v"(xo1), "v"(pw));
+                asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1"
+                    : "=v"(r3) : "v"(xo1), "v"(pw));
+                a0 = *reinterpret_cast<const d2 *>(lds + r0);
+                b0 = *reinterpret_cast<const d2 *>(lds + r1);
+                a1 = *reinterpret_cast<const d2 *>(lds + r2);
+                b1 = *reinterpret_cast<const d2 *>(lds + r3);
             };
-            u4 ln = Lq[0];
+            constexpr unsigned LO = 0x010c000cu, HI = 0x030c020cu;  // rows 0, 1 / rows 2, 3 of the word
+            u2 ln = Lq[0];
             d2 vn[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) vn[q] = Vq[4 * q];
             d2 xa0[4], xa1[4], xc0[4], xc1[4];
-            rdx(ln.x, xa0[0], xa1[0], xa0[1], xa1[1]);
-            rdx(ln.y, xa0[2], xa1[2], xa0[3], xa1[3]);
+            rdx(ln.x, LO, xa0[0], xa1[0], xa0[1], xa1[1]);
+            rdx(ln.x, HI, xa0[2], xa1[2], xa0[3], xa1[3]);
             for (int b = 0; b < nbat; ++b) {
-                rdx(ln.z, xc0[0], xc1[0], xc0[1], xc1[1]);  // second half of batch b
-                rdx(ln.w, xc0[2], xc1[2], xc0[3], xc1[3]);
+                rdx(ln.y, LO, xc0[0], xc1[0], xc0[1], xc1[1]);  // second half of batch b
+                rdx(ln.y, HI, xc0[2], xc1[2], xc0[3], xc1[3]);
                 __builtin_amdgcn_sched_barrier(0);
                 // next batch's offsets (the last batch re-reads itself); volatile
                 // keeps the read here, behind this batch's X reads
                 const int bn = min(b + 1, blast);
-                ln = *(const volatile __attribute__((address_space(3))) u4 *)(Lq + 4 * bn);
+                ln = *(const volatile __attribute__((address_space(3))) u2 *)(Lq + 4 * bn);
                 // the first half's FP64 goes after it: it covers the offsets'
                 // latency before the next batch's X addresses need them
                 __builtin_amdgcn_sched_barrier(0);
@@ -755,8 +774,8 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
 #pragma unroll
                 for (int q = 0; q < 2; ++q)
                     vn[q] = *(const volatile __attribute__((address_space(3))) d2 *)(Vq + 4 * (4 * bn + q));
-                rdx(ln.x, xa0[0], xa1[0], xa0[1], xa1[1]);  // first half of batch b + 1
-                rdx(ln.y, xa0[2], xa1[2], xa0[3], xa1[3]);
+                rdx(ln.x, LO, xa0[0], xa1[0], xa0[1], xa1[1]);  // first half of batch b + 1
+                rdx(ln.x, HI, xa0[2], xa1[2], xa0[3], xa1[3]);
                 __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the second half's FP64
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -781,7 +800,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
                     acc0 = madd(acc0, vn[1].y, xa0[3]);
                     acc1 = madd(acc1, vn[1].y, xa1[3]);
                     if (rem >= 6) {
-                        rdx(ln.z, xc0[0], xc1[0], xc0[1], xc1[1]);
+                        rdx(ln.y, LO, xc0[0], xc1[0], xc0[1], xc1[1]);
                         acc0 = madd(acc0, vn[2].x, xc0[0]);
                         acc1 = madd(acc1, vn[2].x, xc1[0]);
                         acc0 = madd(acc0, vn[2].y, xc0[1]);
@@ -1863,7 +1882,7 @@ struct smfv_plan_s {
     int64_t *direct_off = nullptr;         // per direct row: its first value in tvals
     bool mfma = false;                     // SMFV_PLAN_MFMA: k_rows_mfma (dense blocks) instead of k_rows_ws
     int *mf_rec = nullptr, *mf_ucols = nullptr, *mf_bstep = nullptr;
-    uint16_t *ws_loff = nullptr;
+    uint8_t *ws_loff = nullptr;
     bool k1 = false;                       // K = 1 chunk plan (k_spmv_chunks), ntiles = chunks
     int k1_cap = 0;                        // entry slots per chunk
     int *k1_hdr = nullptr;                 // 4 ints per chunk
@@ -2056,7 +2075,7 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                 p->parts = caps.part_start.size() > 2 ? (int)caps.part_start.size() - 1 : 1;
                 p->union_rows = W.union_rows;
                 p->tiled_nnz = W.tiled_nnz;
-                p->padded_nnz = W.entries;
+                p->padded_nnz = W.ventries;
                 p->ndirect = (int)W.direct.size();
                 p->reuse = W.union_rows ? (double)W.tiled_nnz / (double)W.union_rows : 0.0;
                 if (p->reuse >= SMFV_TILE_MIN_REUSE || (flags & SMFV_PLAN_FORCE_TILES)) {
@@ -2221,7 +2240,7 @@ SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int
     out[1] = (double)W.union_rows;
     out[2] = W.union_rows ? (double)W.tiled_nnz / (double)W.union_rows : 0.0;
     out[3] = (double)W.direct.size();
-    out[4] = (double)W.entries;
+    out[4] = (double)W.ventries;
     out[5] = (double)W.tiled_nnz;
     out[6] = caps.part_start.size() > 2 ? (double)caps.part_start.size() - 1 : 1.0;
     out[7] = footprint;

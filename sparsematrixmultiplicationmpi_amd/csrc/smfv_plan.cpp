@@ -354,18 +354,20 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
         if (r < 0 || r >= m || seen[r]) return fail("direct row out of range or repeated");
         seen[r] = 1;
     }
-    if ((int64_t)P.loff.size() != P.entries + WS_SLACK || P.tsrc.size() != P.loff.size())
+    if ((int64_t)P.loff.size() != P.entries + WS_SLACK || (int64_t)P.tsrc.size() != P.ventries + WS_SLACK)
         return fail("entry arrays");
     // headers and row ownership (sequential: every row in exactly one place)
     for (int t = 0; t < P.ntiles; ++t) {
         const int *g = &P.grec[(size_t)t * WS_GWORDS];
         const int *l = &P.lrec[(size_t)t * WS_LWORDS];
-        const int noff = g[WS_G_NOFF], tn = g[WS_G_TN], nu = g[WS_G_NU];
+        const int noff = g[WS_G_NOFF], tn = g[WS_G_TN], nu = g[WS_G_NU], voff = g[WS_G_VOFF], tnv = g[WS_G_TNV];
         for (int q = 0; q < 16; ++q)
-            if (g[WS_G_NOFF + q] != noff || g[WS_G_TN + q] != tn || g[WS_G_NU + q] != nu)
+            if (g[WS_G_NOFF + q] != noff || g[WS_G_TN + q] != tn || g[WS_G_NU + q] != nu ||
+                g[WS_G_VOFF + q] != voff || g[WS_G_TNV + q] != tnv)
                 return fail("record header not replicated");
         if (noff % 32 || tn % 32 || tn <= 0 || tn > WS_NCAP || nu < 0 || nu > WS_UCAP ||
-            (int64_t)noff + tn > P.entries)
+            (int64_t)noff + tn > P.entries || voff % 8 || tnv % 8 || tnv < 0 || tnv > tn ||
+            (int64_t)voff + tnv > P.ventries)
             return fail("tile header out of range");
         for (int slot = 0; slot < WS_ROWS; ++slot) {
             const int r = l[slot];
@@ -383,11 +385,11 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
     auto check_tile = [&](int t) -> const char * {
         const int *g = &P.grec[(size_t)t * WS_GWORDS];
         const int *l = &P.lrec[(size_t)t * WS_LWORDS];
-        const int noff = g[WS_G_NOFF], tn = g[WS_G_TN], nu = g[WS_G_NU];
+        const int noff = g[WS_G_NOFF], tn = g[WS_G_TN], nu = g[WS_G_NU], voff = g[WS_G_VOFF], tnv = g[WS_G_TNV];
         for (int q = 0; q < 256; ++q)
             if (g[q] < 0 || g[q] >= n) return "union id out of range";
         for (int e = noff; e < noff + tn; ++e)
-            if (P.loff[e] != WS_ZOFF && (P.loff[e] % 256 || P.loff[e] / 256 >= nu))
+            if (P.loff[e] != WS_UCAP && P.loff[e] >= nu)
                 return "entry offset outside the tile's union";
         for (int slot = 0; slot < WS_ROWS; ++slot) {
             const int r = l[slot];
@@ -396,19 +398,27 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
             const int k = (slot >> 3) & 3;
             const int rl = rp[r + 1] - rp[r];
             if (len % 2 || len < rl || len > rl + 1) return "row segment length";
+            // the entries the kernel sums (len: the row's, rounded up to even);
+            // past them its reads only prefetch (never summed), so a quad's
+            // last batch may store fewer value pairs than offsets
             for (int b = 0; b < (len + 7) / 8; ++b)
                 for (int u = 0; u < 8; ++u) {
                     const int el = 8 * b + u;
                     const int64_t le = (int64_t)noff + (int64_t)(lb + 4 * b + k) * 8 + u;
-                    const int64_t ve = (int64_t)noff + (int64_t)(vb + 4 * (4 * b + u / 2) + k) * 2 + u % 2;
-                    if (le >= noff + tn || ve >= noff + tn) return "segment leaves its tile";
+                    const int64_t ve = (int64_t)voff + (int64_t)(vb + 4 * (4 * b + u / 2) + k) * 2 + u % 2;
+                    if (le >= noff + tn) return "segment leaves its tile";
+                    if (el >= len) {  // never summed: the offset only has to stay on the zero row
+                        if (P.loff[le] != WS_UCAP) return "prefetched pad offset not on the zero row";
+                        continue;
+                    }
+                    if (ve >= voff + tnv) return "segment leaves its tile";
                     if (el < rl) {
                         const int j = rp[r] + el;
-                        const int u_ = P.loff[le] / 256;
+                        const int u_ = P.loff[le];
                         const int w = (u_ / 4) / 8, i = (u_ / 4) % 8, qq = u_ % 4;
-                        if (P.tsrc[ve] != j || P.loff[le] == WS_ZOFF || u_ >= nu || g[32 * w + 8 * qq + i] != ci[j])
+                        if (P.tsrc[ve] != j || P.loff[le] == WS_UCAP || u_ >= nu || g[32 * w + 8 * qq + i] != ci[j])
                             return "row entry is not its CSR non-zero";
-                    } else if (P.tsrc[ve] != -1 || P.loff[le] != WS_ZOFF) {
+                    } else if (P.tsrc[ve] != -1 || P.loff[le] != WS_UCAP) {
                         return "pad entry does not read the zero row";
                     }
                 }
@@ -522,10 +532,25 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         for (size_t q = 0; q < rows.size(); q += 4) e += 4 * (int64_t)len8(rows[q]);
         return e;
     };
+    // value entries of a quad: its offsets' 32 per batch, less the value
+    // pairs of its last batch that no row sums (pair groups q >= qmax of a
+    // batch sit last in the quad's value range: rows of 27 store 28, not 32)
+    auto vquad = [&](const std::vector<int> &rows, size_t q0) {
+        const int nb = len8(rows[q0]) / 8;
+        int qmax = 0;
+        for (size_t k = q0; k < q0 + 4 && k < rows.size(); ++k)
+            if (len8(rows[k]) / 8 == nb) qmax = std::max(qmax, (len2(rows[k]) - 8 * (nb - 1) + 1) / 2);
+        return 32 * (int64_t)nb - 8 * (int64_t)(4 - qmax);
+    };
+    auto vlayout = [&](const std::vector<int> &rows) {
+        int64_t e = 0;
+        for (size_t q = 0; q < rows.size(); q += 4) e += vquad(rows, q);
+        return e;
+    };
     // one tile into the plan at entry offset noff, record index t (the
     // tiles are independent: run in parallel, each with its own pos stamps)
-    auto emit = [&](const std::vector<int> &R, int64_t noff, int t, std::vector<int> &pos, std::vector<int> &ucols,
-                    int64_t &tiled, int64_t &unions) {
+    auto emit = [&](const std::vector<int> &R, int64_t noff, int64_t vnoff, int t, std::vector<int> &pos,
+                    std::vector<int> &ucols, int64_t &tiled, int64_t &unions) {
         ucols.clear();
         for (int r : R)
             for (int j = rp[r]; j < rp[r + 1]; ++j)
@@ -537,18 +562,18 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         int *lrec = &P.lrec[(size_t)t * WS_LWORDS];
         int *grec = &P.grec[(size_t)t * WS_GWORDS];
         for (int s = 0; s < WS_ROWS; ++s) lrec[s] = -1;
-        int64_t e = 0;
+        int64_t e = 0, ev = 0;
         for (int q = 0; 4 * q < (int)R.size(); ++q) {
             const int o = q / 2, w = o < 4 ? o : 11 - o, h = q % 2;  // octet o -> wave; SIMD s runs octets s and 7 - s
             const int nb = len8(R[4 * q]) / 8;
-            const int lbase = (int)(e / 8), vbase = (int)(e / 2);
+            const int lbase = (int)(e / 8), vbase = (int)(ev / 2);
             for (int k = 0; k < 4 && 4 * q + k < (int)R.size(); ++k) {
                 const int r = R[4 * q + k], slot = (4 * h + k) * 8 + w;
                 for (int j = rp[r]; j < rp[r + 1]; ++j) {
                     const int el = j - rp[r];
                     P.loff[(size_t)(noff + (int64_t)(lbase + 4 * (el / 8) + k) * 8 + el % 8)] =
-                        (uint16_t)(pos[ci[j]] * 256);
-                    P.tsrc[(size_t)(noff + (int64_t)(vbase + 4 * (el / 2) + k) * 2 + el % 2)] = j;
+                        (uint8_t)pos[ci[j]];
+                    P.tsrc[(size_t)(vnoff + (int64_t)(vbase + 4 * (el / 2) + k) * 2 + el % 2)] = j;
                 }
                 lrec[slot] = r;
                 lrec[64 + slot] = lbase | (len2(r) << 16);
@@ -556,6 +581,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
                 tiled += rp[r + 1] - rp[r];
             }
             e += 32 * nb;
+            ev += vquad(R, (size_t)(4 * q));
         }
         for (int w = 0; w < WS_LOADERS; ++w)
             for (int q = 0; q < 4; ++q)
@@ -567,6 +593,8 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
             grec[WS_G_NOFF + q] = (int)noff;
             grec[WS_G_TN + q] = (int)e;
             grec[WS_G_NU + q] = nu;
+            grec[WS_G_VOFF + q] = (int)vnoff;
+            grec[WS_G_TNV + q] = (int)ev;
         }
         for (int c : ucols) pos[c] = -1;
         unions += nu;
@@ -659,19 +687,21 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     // each tile's entry offset (a prefix sum of its quad layout), then the
     // tiles emitted in parallel into their own ranges
     const int nt = (int)tiles.size();
-    std::vector<int64_t> toff((size_t)nt + 1, 0);
+    std::vector<int64_t> toff((size_t)nt + 1, 0), tvoff((size_t)nt + 1, 0);
     for (int t = 0; t < nt; ++t) {
         by_length(tiles[(size_t)t]);
         toff[(size_t)t + 1] = toff[(size_t)t] + layout(tiles[(size_t)t]);
+        tvoff[(size_t)t + 1] = tvoff[(size_t)t] + vlayout(tiles[(size_t)t]);
     }
     P.ntiles = nt;
     P.entries = toff[(size_t)nt];
+    P.ventries = tvoff[(size_t)nt];
     if (P.entries + WS_SLACK > 0x7fffffff) {
         if (err) *err = "ws plan: too many tile entries for int32 offsets";
         return false;
     }
-    P.loff.assign((size_t)(P.entries + WS_SLACK), (uint16_t)WS_ZOFF);
-    P.tsrc.assign((size_t)(P.entries + WS_SLACK), -1);
+    P.loff.assign((size_t)(P.entries + WS_SLACK), (uint8_t)WS_UCAP);
+    P.tsrc.assign((size_t)(P.ventries + WS_SLACK), -1);
     P.grec.assign((size_t)nt * WS_GWORDS, 0);
     P.lrec.assign((size_t)nt * WS_LWORDS, 0);
     {
@@ -681,7 +711,8 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         auto work = [&](int w) {
             std::vector<int> pos((size_t)std::max(n, 1), -1), ucols;
             for (int t = (int)((int64_t)nt * w / nth); t < (int)((int64_t)nt * (w + 1) / nth); ++t)
-                emit(tiles[(size_t)t], toff[(size_t)t], t, pos, ucols, tiled[(size_t)w], unions[(size_t)w]);
+                emit(tiles[(size_t)t], toff[(size_t)t], tvoff[(size_t)t], t, pos, ucols, tiled[(size_t)w],
+                     unions[(size_t)w]);
         };
         std::vector<std::thread> pool;
         for (int w = 1; w < nth; ++w) pool.emplace_back(work, w);

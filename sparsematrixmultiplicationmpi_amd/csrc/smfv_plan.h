@@ -28,15 +28,16 @@ constexpr int TILE_KP = 32;
 // base + 4c + k) so one meta read of a lane group touches four bank groups.
 // ---------------------------------------------------------------------------
 constexpr int WS_UCAP = 239;     // union rows per tile
-constexpr int WS_NCAP = 1792;    // LDS entries per tile (u16 offset + f64 value)
+constexpr int WS_NCAP = 1792;    // LDS entries per tile (u8 image row + f64 value)
 constexpr int WS_ROWS = 64;      // rows per tile
 constexpr int WS_LOADERS = 8;    // loader waves; each stages 8 x 1 KiB of X
 constexpr int WS_ZOFF = WS_UCAP * 256;  // byte offset of the zero row
 // global record (per tile, int32): [0, 256) union ids in loader-lane order
 // (loader wave w, lane quarter q, piece i -> union id 4 * (8w + i) + q at
-// word 32w + 8q + i), then noff / tn / nu, each replicated 16x so any lane
-// reads its copy with no broadcast
-constexpr int WS_GWORDS = 320, WS_G_NOFF = 256, WS_G_TN = 272, WS_G_NU = 288;
+// word 32w + 8q + i), then noff / tn / nu (the tile's offsets: first entry,
+// entries; its union rows) and voff / tnv (its values: first entry, entries),
+// each replicated 16x so any lane reads its copy with no broadcast
+constexpr int WS_GWORDS = 352, WS_G_NOFF = 256, WS_G_TN = 272, WS_G_NU = 288, WS_G_VOFF = 304, WS_G_TNV = 320;
 // LDS record (per tile, 256 int32 = 1 KiB): [0, 64) row per team slot (-1 none),
 // [64, 128) L chunk base | (padded length << 16), [128, 192) V chunk base;
 // team slot = team-in-wave * 8 + wave
@@ -107,12 +108,14 @@ struct WsPlan {
     int ntiles = 0;
     std::vector<int> grec;         // WS_GWORDS per tile
     std::vector<int> lrec;         // WS_LWORDS per tile
-    std::vector<uint16_t> loff;    // per entry: byte offset of its X row in the LDS image
-    std::vector<int> tsrc;         // per entry: CSR index of its value (-1: pad)
+    std::vector<uint8_t> loff;     // per offset entry: its X row in the LDS image (union position; WS_UCAP: pad)
+    std::vector<int> tsrc;         // per value entry: CSR index of its value (-1: pad)
     std::vector<int> direct;       // rows over a cap alone, gathered straight from X
     int64_t union_rows = 0;        // X rows staged per 32-column panel
     int64_t tiled_nnz = 0;         // non-zeros in tiles (not direct)
-    int64_t entries = 0;           // used length of loff / tsrc (the vectors carry WS_SLACK more)
+    int64_t entries = 0;           // used length of loff (the vector carries WS_SLACK more)
+    int64_t ventries = 0;          // used length of tsrc (the vector carries WS_SLACK more): a quad's
+                                   // last batch stores only the value pairs its rows use
     int xcd[9] = {};               // XCD x runs tiles [xcd[x], xcd[x + 1])
 };
 

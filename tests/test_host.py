@@ -225,6 +225,22 @@ def _analyse_rows(A, r0, r1, flags=0):
             "footprint": out[7], "xcd_footprint": out[8]}
 
 
+def test_ws_plan_tiny_and_empty_rows():
+    """The headline kernel's tile plan (built and verified natively) on tiny
+    and empty-row patterns: a tile of empty rows stages no values (a quad's
+    last batch stores only the value pairs its rows sum), and the value
+    entries never exceed 8 per non-zero rounded up per batch."""
+    for name in ("empty7x5.mtx", "pat4x6.mtx"):
+        A = smfv.readMatrixMarketFile(os.path.join(GOLDEN, name))
+        out = (ctypes.c_double * 9)()
+        ip = ctypes.POINTER(ctypes.c_int)
+        _lib.call("smfv_plan_analyse_rows", 0, A.numRows, A.numCols, A.rowPtr.ctypes.data_as(ip),
+                  A.colIndices.ctypes.data_as(ip), 0, out)
+        assert out[0] >= 1, name
+        nnz = int(A.rowPtr[-1])
+        assert out[5] == nnz and out[4] % 8 == 0 and nnz <= out[4] <= 32 * A.numRows, (name, list(out))
+
+
 def test_xcd_parts_cut_compulsory_x_traffic():
     """Each XCD has its own L2: the plan splits the rows into 8 parts (row
     ranges or breadth-first shares, whichever reads fewer X rows) and runs
