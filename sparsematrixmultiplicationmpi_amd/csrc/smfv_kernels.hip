@@ -1833,6 +1833,11 @@ static TileCaps plan_caps(int flags, int col_base)
     caps.frontier = !(flags & SMFV_PLAN_NATURAL_SEEDS);
     caps.split_ends = (flags & SMFV_PLAN_SPLIT_ENDS) ? SMFV_WS_BLOCKS_PER_XCD : 0;
     caps.col_base = col_base;  // a row block's neighbours are its columns shifted by its first global row
+#ifdef SMFV_LAB
+    // lab: smaller tiles (rows / entries / union) to measure what a unit costs
+    if (const char *e = std::getenv("SMFV_WS_MAXROWS")) caps.maxrows = std::max(8, std::min(WS_ROWS, atoi(e)));
+    if (const char *e = std::getenv("SMFV_WS_UCAP")) caps.ucap = std::max(8, std::min(WS_UCAP, atoi(e)));
+#endif
     return caps;
 }
 
