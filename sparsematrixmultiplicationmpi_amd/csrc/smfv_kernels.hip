@@ -2505,7 +2505,8 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
                   : abl == 13 ? k_rows_ws_lab<13> : abl == 14 ? k_rows_ws_lab<14> : abl == 15 ? k_rows_ws_lab<15> : abl == 16 ? k_rows_ws_lab<16>
                   : abl == 9 ? (K == TILE_KP ? k_rows_ws_lab<9> : k_rows_ws<>)
                   : abl == 10 ? (K == TILE_KP ? k_rows_ws_lab<10> : k_rows_ws<>)
-                  : abl == 11 ? (K == TILE_KP ? k_rows_ws_lab<11> : k_rows_ws<>) : k_rows_ws<>;
+                  : abl == 11 ? (K == TILE_KP ? k_rows_ws_lab<11> : k_rows_ws<>)
+                  : abl == 17 ? (K == TILE_KP && plan->m >= 120000 ? k_rows_ws_lab<17> : k_rows_ws<>) : k_rows_ws<>;
         if (!(saddr && lab_saddr)) kern = plan->fma ? k_rows_ws<true, false> : k_rows_ws<false, false>;
         static unsigned long long *stamp_buf = nullptr;
         const size_t stamp_n = (size_t)blocks * 16 * WS_STAMP_UNITS * 2;
