@@ -23,9 +23,10 @@ constexpr int TILE_KP = 32;
 // Rows are sorted by decreasing length and dealt in quads (4 teams of one
 // lane group, similar lengths), two quads (8 consecutive rows) per compute
 // wave, and the waves sharing a SIMD (w, w + 4) take a long and a short
-// octet; a quad's entries are interleaved in 16-byte
-// chunks (batch b of team k at chunk base + 4b + k, value pair c at chunk
-// base + 4c + k) so one meta read of a lane group touches four bank groups.
+// octet; a quad's entries are interleaved (the 8 u8 image rows of batch b of
+// team k in the 8-byte chunk base + 4b + k, value pair c of team k in the
+// 16-byte chunk base + 4c + k) so one meta read of a lane group touches four
+// bank groups; a quad's value range ends after the last pair its rows sum.
 // ---------------------------------------------------------------------------
 constexpr int WS_UCAP = 239;     // union rows per tile
 constexpr int WS_NCAP = 1792;    // LDS entries per tile (u8 image row + f64 value)
