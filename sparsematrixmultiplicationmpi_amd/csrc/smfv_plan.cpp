@@ -20,6 +20,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <functional>
 #include <thread>
 
 namespace smfv {
@@ -549,8 +550,9 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     };
     // one tile into the plan at entry offset noff, record index t (the
     // tiles are independent: run in parallel, each with its own pos stamps)
+    std::vector<std::vector<int>> tunion;  // each tile's union rows (filled before the emit)
     auto emit = [&](const std::vector<int> &R, int64_t noff, int64_t vnoff, int t, std::vector<int> &pos,
-                    std::vector<int> &ucols, int64_t &tiled, int64_t &unions) {
+                    std::vector<int> &stamp, std::vector<int> &ucols, int64_t &tiled, int64_t &unions) {
         ucols.clear();
         for (int r : R)
             for (int j = rp[r]; j < rp[r + 1]; ++j)
@@ -559,6 +561,28 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
                     ucols.push_back(ci[j]);
                 }
         const int nu = (int)ucols.size();
+        // issue order: the loaders issue piece i of every wave before piece
+        // i + 1, so the union rows no tile of the XCD's previous two strides
+        // staged (likely HBM, not L2) take the positions issued first
+        if (nu > 4) {
+            int x = 0;
+            while (x < 7 && t >= P.xcd[x + 1]) ++x;
+            const int first = P.xcd[x], nb = std::max(1, caps.xcd_blocks);
+            const int lo = std::max(first, t - (t - first) % nb - 2 * nb), hi = t - (t - first) % nb;
+            for (int t2 = lo; t2 < hi; ++t2)
+                for (int c : tunion[(size_t)t2]) stamp[c] = t;
+            std::vector<int> cold, warm;
+            for (int c : ucols) (stamp[c] == t ? warm : cold).push_back(c);
+            cold.insert(cold.end(), warm.begin(), warm.end());
+            int k = 0;
+            for (int i = 0; i < 8; ++i)
+                for (int w = 0; w < WS_LOADERS; ++w)
+                    for (int q = 0; q < 4; ++q) {
+                        const int u = 4 * (8 * w + i) + q;
+                        if (u < nu) ucols[(size_t)u] = cold[(size_t)k++];
+                    }
+            for (int u = 0; u < nu; ++u) pos[ucols[(size_t)u]] = u;
+        }
         int *lrec = &P.lrec[(size_t)t * WS_LWORDS];
         int *grec = &P.grec[(size_t)t * WS_GWORDS];
         for (int s = 0; s < WS_ROWS; ++s) lrec[s] = -1;
@@ -708,16 +732,26 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         const int nth = std::max(1, std::min({8, (nt + 63) / 64, (int)std::max(1u, std::thread::hardware_concurrency()),
                                               analysis_threads > 0 ? analysis_threads : 8}));
         std::vector<int64_t> tiled((size_t)nth, 0), unions((size_t)nth, 0);
-        auto work = [&](int w) {
-            std::vector<int> pos((size_t)std::max(n, 1), -1), ucols;
+        tunion.assign((size_t)nt, {});
+        auto unite = [&](int w) {
+            std::vector<int> seen((size_t)std::max(n, 1), -1);
             for (int t = (int)((int64_t)nt * w / nth); t < (int)((int64_t)nt * (w + 1) / nth); ++t)
-                emit(tiles[(size_t)t], toff[(size_t)t], tvoff[(size_t)t], t, pos, ucols, tiled[(size_t)w],
+                for (int r : tiles[(size_t)t])
+                    for (int j = rp[r]; j < rp[r + 1]; ++j)
+                        if (seen[ci[j]] != t) seen[ci[j]] = t, tunion[(size_t)t].push_back(ci[j]);
+        };
+        auto work = [&](int w) {
+            std::vector<int> pos((size_t)std::max(n, 1), -1), stamp((size_t)std::max(n, 1), -1), ucols;
+            for (int t = (int)((int64_t)nt * w / nth); t < (int)((int64_t)nt * (w + 1) / nth); ++t)
+                emit(tiles[(size_t)t], toff[(size_t)t], tvoff[(size_t)t], t, pos, stamp, ucols, tiled[(size_t)w],
                      unions[(size_t)w]);
         };
-        std::vector<std::thread> pool;
-        for (int w = 1; w < nth; ++w) pool.emplace_back(work, w);
-        work(0);
-        for (auto &x : pool) x.join();
+        for (auto fn : {std::function<void(int)>(unite), std::function<void(int)>(work)}) {
+            std::vector<std::thread> pool;
+            for (int w = 1; w < nth; ++w) pool.emplace_back(fn, w);
+            fn(0);
+            for (auto &x : pool) x.join();
+        }
         for (int w = 0; w < nth; ++w) P.tiled_nnz += tiled[(size_t)w], P.union_rows += unions[(size_t)w];
     }
     tick("emit");
