@@ -657,7 +657,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
             };
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                const int piece = 8 * wl + i;  // 1 KiB = union rows 4*piece .. +3
+                const int piece = wl + 8 * i;  // 1 KiB = union rows 4*piece .. +3 (pieces dealt round-robin)
                 const int u = 4 * piece + (lane >> 4);
                 if (4 * piece < nu && u < WS_UCAP) {
                     if constexpr (SADDR)
@@ -2257,7 +2257,7 @@ SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int
         for (int t = W.xcd[x]; t < W.xcd[x + 1]; ++t) {
             const int *G = &W.grec[(size_t)t * WS_GWORDS];
             for (int u = 0; u < G[WS_G_NU]; ++u) {
-                const int c = G[32 * ((u / 4) / 8) + 8 * (u % 4) + (u / 4) % 8];
+                const int c = G[32 * ((u / 4) % 8) + 8 * (u % 4) + (u / 4) / 8];
                 if (stamp[c] != x) stamp[c] = x, ++sum;
             }
         }

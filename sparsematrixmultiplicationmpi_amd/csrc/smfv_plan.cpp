@@ -416,7 +416,7 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
                     if (el < rl) {
                         const int j = rp[r] + el;
                         const int u_ = P.loff[le];
-                        const int w = (u_ / 4) / 8, i = (u_ / 4) % 8, qq = u_ % 4;
+                        const int w = (u_ / 4) % 8, i = (u_ / 4) / 8, qq = u_ % 4;
                         if (P.tsrc[ve] != j || P.loff[le] == WS_UCAP || u_ >= nu || g[32 * w + 8 * qq + i] != ci[j])
                             return "row entry is not its CSR non-zero";
                     } else if (P.tsrc[ve] != -1 || P.loff[le] != WS_UCAP) {
@@ -561,9 +561,10 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
                     ucols.push_back(ci[j]);
                 }
         const int nu = (int)ucols.size();
-        // issue order: the loaders issue piece i of every wave before piece
-        // i + 1, so the union rows no tile of the XCD's previous two strides
-        // staged (likely HBM, not L2) take the positions issued first
+        // issue order: loader wave w stages pieces w, w + 8, ... (4 union
+        // rows each) in that order, so positions go out in ascending order;
+        // the union rows no tile of the XCD's previous two strides staged
+        // (likely HBM, not L2) take the first ones
         if (nu > 4) {
             int x = 0;
             while (x < 7 && t >= P.xcd[x + 1]) ++x;
@@ -574,13 +575,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
             std::vector<int> cold, warm;
             for (int c : ucols) (stamp[c] == t ? warm : cold).push_back(c);
             cold.insert(cold.end(), warm.begin(), warm.end());
-            int k = 0;
-            for (int i = 0; i < 8; ++i)
-                for (int w = 0; w < WS_LOADERS; ++w)
-                    for (int q = 0; q < 4; ++q) {
-                        const int u = 4 * (8 * w + i) + q;
-                        if (u < nu) ucols[(size_t)u] = cold[(size_t)k++];
-                    }
+            ucols.swap(cold);
             for (int u = 0; u < nu; ++u) pos[ucols[(size_t)u]] = u;
         }
         int *lrec = &P.lrec[(size_t)t * WS_LWORDS];
@@ -610,7 +605,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         for (int w = 0; w < WS_LOADERS; ++w)
             for (int q = 0; q < 4; ++q)
                 for (int i = 0; i < 8; ++i) {
-                    const int u = 4 * (8 * w + i) + q;
+                    const int u = 4 * (w + 8 * i) + q;
                     grec[32 * w + 8 * q + i] = u < nu ? ucols[u] : 0;
                 }
         for (int q = 0; q < 16; ++q) {

@@ -34,8 +34,8 @@ constexpr int WS_ROWS = 64;      // rows per tile
 constexpr int WS_LOADERS = 8;    // loader waves; each stages 8 x 1 KiB of X
 constexpr int WS_ZOFF = WS_UCAP * 256;  // byte offset of the zero row
 // global record (per tile, int32): [0, 256) union ids in loader-lane order
-// (loader wave w, lane quarter q, piece i -> union id 4 * (8w + i) + q at
-// word 32w + 8q + i), then noff / tn / nu (the tile's offsets: first entry,
+// (loader wave w, lane quarter q, its i-th piece -> union id 4 * (w + 8i) + q
+// at word 32w + 8q + i), then noff / tn / nu (the tile's offsets: first entry,
 // entries; its union rows) and voff / tnv (its values: first entry, entries),
 // each replicated 16x so any lane reads its copy with no broadcast
 constexpr int WS_GWORDS = 352, WS_G_NOFF = 256, WS_G_TN = 272, WS_G_NU = 288, WS_G_VOFF = 304, WS_G_TNV = 320;
