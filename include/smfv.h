@@ -188,6 +188,14 @@ typedef struct smfv_plan_s *smfv_plan_t;
 /* The former tiled kernel (k_rows_ws: ~60-row tiles whose whole X union sits
  * in LDS) where SMFV_PLAN_CS would be the default (A/B). */
 #define SMFV_PLAN_WS 512
+/* (r4) The geometry of k_rows_ws (A/B; without either flag the library's
+ * default): GEOM1 one 1024-lane block per CU (8 compute + 8 loader waves,
+ * tiles of <= 64 rows and <= 239 staged X rows, 158 KiB of LDS); GEOM2 two
+ * independent 512-lane blocks per CU (4 + 4 waves, tiles of <= 32 rows and
+ * <= 125 X rows, 80 KiB of LDS each), so one block's per-tile hand-off hides
+ * behind the other's work.  Same per-row order: bit-identical either way. */
+#define SMFV_PLAN_WS_GEOM1 1024
+#define SMFV_PLAN_WS_GEOM2 2048
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
 /* Plan of the row block [row_begin, row_end) of a CSR matrix (h_row_ptr /
@@ -249,8 +257,9 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
  * rows per XCD, 1: one wavefront), [12] X rows the 8 parts read, summed,
  * over the pattern's X rows (-1: not computed), [13] the kernel a tiled
  * plan runs: 0 none (untiled), 1 k_rows_ws, 2 k_rows_mfma, 3 k_spmv_chunks,
- * 4 k_rows_cs; [14] chunks of a k_rows_cs plan */
-#define SMFV_PLAN_STATS 15
+ * 4 k_rows_cs; [14] chunks of a k_rows_cs plan; [15] (r4) the k_rows_ws
+ * geometry (1: one 1024-lane block per CU, 2: two 512-lane blocks; 0 other) */
+#define SMFV_PLAN_STATS 16
 SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS]);
 SMFV_API int smfv_plan_destroy(smfv_plan_t plan);
 

@@ -556,6 +556,26 @@ template <bool NT> __device__ __forceinline__ void dma16s(const void *base, unsi
                      : "=&s"(keep) : "v"(voff), "s"(sb), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
 }
 __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// (r4) LDS layout of a k_rows_ws geometry (WsGeom, smfv_plan.h): two X
+// images of UCAP + 1 rows (the last one zero), then two meta slots of values,
+// u8 offsets and the tile's record ([0, R) rows, [R, 2R) L bases, [2R, 3R) V
+// bases; 1 KiB for 64-row tiles, 384 B rounded to 512 for 32-row tiles)
+template <int CW, int LW, int UCAP, int NCAP> struct Lay {
+    static constexpr int R = 8 * CW;
+    static constexpr int XSLOT = (UCAP + 1) * 256;
+    static constexpr int SL_M = 2 * XSLOT;
+    static constexpr int M_V = 0, M_L = (NCAP + 127) / 128 * 1024, M_R = M_L + (NCAP + 1023) / 1024 * 1024;
+    static constexpr int REC_LANES = CW == 8 ? 64 : 3 * R / 4;  // 16 B per lane
+    static constexpr int RECB = CW == 8 ? 1024 : (REC_LANES * 16 + 255) / 256 * 256;
+    static constexpr int MSLOT = M_R + RECB;
+    static constexpr int BYTES = SL_M + 2 * MSLOT;
+    static constexpr int ZOFF = UCAP * 256;
+    static_assert(BYTES <= (CW == 8 ? 160 : 80) * 1024, "the blocks of one CU share its 160 KiB");
+    static_assert(UCAP + 1 <= 4 * 8 * LW, "8 X pieces per loader wave cover the image");
+    static_assert(UCAP <= 255, "u8 image offsets");
+    static_assert(XSLOT % 16 == 0 && MSLOT % 16 == 0 && M_L % 1024 == 0, "16-byte DMA lanes");
+};
 }  // namespace ws
 
 // SADDR: the loaders address X, the values and the offsets by scalar base +
@@ -563,8 +583,8 @@ __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(
 struct WsXcd {
     int first[9];  // XCD x runs tiles [first[x], first[x + 1]) of the plan's order
 };
-template <bool FMA = false, bool SADDR = true>
-__global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int chunked,
+template <int CW, int LW, int UCAP, int NCAP, bool FMA = false, bool SADDR = true>
+__global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsXcd xr, int npanel, int chunked,
                                                      const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
                                                      const uint8_t *__restrict__ loff,
@@ -573,7 +593,9 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
                                                      double *__restrict__ Y, int64_t ldy)
 {
     using namespace ws;
-    __shared__ __attribute__((aligned(16))) char lds[SL_M + 2 * MSLOT];
+    using L = Lay<CW, LW, UCAP, NCAP>;
+    constexpr int XSLOT = L::XSLOT, SL_M = L::SL_M, M_V = L::M_V, M_L = L::M_L, M_R = L::M_R, MSLOT = L::MSLOT;
+    __shared__ __attribute__((aligned(16))) char lds[L::BYTES];
     int t0, tstep, cnt;
     {
         // XCD x = blockIdx.x % 8 owns tiles [first, end) of the plan's order
@@ -601,14 +623,14 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
     const int nunits = cnt * npanel;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const unsigned lds0 = (unsigned)(uintptr_t)lds;  // LDS byte address of the block's image
-    if (wv >= 8) {
+    if (wv >= CW) {
         // ---------------- loader waves ----------------
         // loaders win instruction arbitration on their SIMD: a DMA issued
         // late stretches the whole unit (30.1 -> 28.0 us on the surrogate)
         __builtin_amdgcn_s_setprio(3);
-        const int wl = wv - 8;
+        const int wl = wv - CW;
         if (wl == 0 && lane < 32)  // zero row of both X slots
-            reinterpret_cast<d2 *>(lds + (lane >> 4) * XSLOT + WS_ZOFF)[lane & 15] = d2{0.0, 0.0};
+            reinterpret_cast<d2 *>(lds + (lane >> 4) * XSLOT + L::ZOFF)[lane & 15] = d2{0.0, 0.0};
         i4 u0, u1;
         int noff, tn, nu, voff, tnv;
         unsigned xo[8];                       // SADDR: byte offset of this lane's 16 B of union row uc[i]
@@ -642,24 +664,26 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
                     const int nf = __builtin_amdgcn_readfirstlane(noff);
                     const double *tvb = tv + __builtin_amdgcn_readfirstlane(voff);
                     const uint8_t *lb = loff + nf;
-                    for (int k = wl; k * 128 < tnv; k += WS_LOADERS)
+                    for (int k = wl; k * 128 < tnv; k += LW)
                         dma16s<true>(tvb, 1024u * k + 16u * lane, mb + M_V + k * 1024);
-                    for (int k = wl; k * 1024 < tn; k += WS_LOADERS)
+                    for (int k = wl; k * 1024 < tn; k += LW)
                         dma16s<true>(lb, 1024u * k + 16u * lane, mb + M_L + k * 1024);
-                    if (wl == WS_LOADERS - 1) dma16s<true>(lrec + (int64_t)t * WS_LWORDS, 16u * lane, mb + M_R);
+                    if (wl == LW - 1 && lane < L::REC_LANES)
+                        dma16s<true>(lrec + (int64_t)t * WS_LWORDS, 16u * lane, mb + M_R);
                 } else {
-                    for (int k = wl; k * 128 < tnv; k += WS_LOADERS)
+                    for (int k = wl; k * 128 < tnv; k += LW)
                         dma16<true>(tv + voff + 128 * k + 2 * lane, mb + M_V + k * 1024);
-                    for (int k = wl; k * 1024 < tn; k += WS_LOADERS)
+                    for (int k = wl; k * 1024 < tn; k += LW)
                         dma16<true>(loff + noff + 1024 * k + 16 * lane, mb + M_L + k * 1024);
-                    if (wl == WS_LOADERS - 1) dma16<true>(lrec + (int64_t)t * WS_LWORDS + 4 * lane, mb + M_R);
+                    if (wl == LW - 1 && lane < L::REC_LANES)
+                        dma16<true>(lrec + (int64_t)t * WS_LWORDS + 4 * lane, mb + M_R);
                 }
             };
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                const int piece = wl + 8 * i;  // 1 KiB = union rows 4*piece .. +3 (pieces dealt round-robin)
+                const int piece = wl + LW * i;  // 1 KiB = union rows 4*piece .. +3 (pieces dealt round-robin)
                 const int u = 4 * piece + (lane >> 4);
-                if (4 * piece < nu && u < WS_UCAP) {
+                if (4 * piece < nu && u < UCAP) {
                     if constexpr (SADDR)
                         dma16s<false>(X + cp, xo[i], xb + piece * 1024);
                     else
@@ -699,7 +723,7 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
             return a + v * x;
     };
     const int tw = (tid >> 3) & 7, tl = tid & 7, par = tw & 1;
-    const int slot = tw * 8 + wv;
+    const int slot = tw * CW + wv;
     const int qk = tw & 3;  // position of the team in its quad
     barrier_lds();
     int it = 0, p = 0;
@@ -709,13 +733,13 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
         const int *R = reinterpret_cast<const int *>(mbase + M_R);
         const int row = R[slot];
         if (row >= 0) {
-            const int info = R[64 + slot];
+            const int info = R[L::R + slot];
             // the row runs nbat whole batches of 8, then rem (0, 2, 4 or 6)
             // entries of one more (its length rounded up to even)
             const int js = info & 0xFFFF, len = info >> 16, nbat = len >> 3, rem = len & 7;
             const int blast = nbat + (rem ? 1 : 0) - 1;
             const u2 *Lq = reinterpret_cast<const u2 *>(mbase + M_L) + js + qk;
-            const d2 *Vq = reinterpret_cast<const d2 *>(mbase + M_V) + R[128 + slot] + qk;
+            const d2 *Vq = reinterpret_cast<const d2 *>(mbase + M_V) + R[2 * L::R + slot] + qk;
             const char *xb0 = xbase + par * 128 + tl * 16;
             const char *xb1 = xbase + (par ^ 1) * 128 + tl * 16;
             d2 acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0};
@@ -823,6 +847,18 @@ __global__ __launch_bounds__(1024, 1) void k_rows_ws(WsXcd xr, int npanel, int c
 #ifdef SMFV_LAB
 #include "lab/ws_lab.inc"  // the instrumented lab copy (libsmfv_lab.so only)
 #endif
+
+// the product instances of k_rows_ws: geometry (smfv_plan.h WsGeom) x FMA x SADDR
+template <bool FMA, bool SADDR>
+constexpr auto WS1 = k_rows_ws<WS_GEOM1.cw, WS_GEOM1.lw, WS_GEOM1.ucap, WS_GEOM1.ncap, FMA, SADDR>;
+template <bool FMA, bool SADDR>
+constexpr auto WS2 = k_rows_ws<WS_GEOM2.cw, WS_GEOM2.lw, WS_GEOM2.ucap, WS_GEOM2.ncap, FMA, SADDR>;
+static auto pick_ws(int geom, bool fma, bool saddr)
+{
+    if (geom == 2)
+        return fma ? (saddr ? WS2<true, true> : WS2<true, false>) : (saddr ? WS2<false, true> : WS2<false, false>);
+    return fma ? (saddr ? WS1<true, true> : WS1<true, false>) : (saddr ? WS1<false, true> : WS1<false, false>);
+}
 
 // ---------------------------------------------------------------------------
 // k_rows_cs: column-streamed tiles (K % 32 == 0; plan build_cs_plan).
@@ -1822,7 +1858,8 @@ constexpr double SMFV_TILE_MIN_REUSE = 3.0;
 // rows' own sub-pattern misjudges a permuted matrix).
 constexpr int SMFV_TILE_SAMPLE_TILES = 128;  // (r3: 512 -> 128, 1/4 of the sample's time; 8k rows decide >= 3)
 constexpr int SMFV_TILE_SAMPLE_MIN_ROWS = 16384;  // below this the full analysis runs directly
-constexpr int SMFV_WS_BLOCKS_PER_XCD = 32;        // k_rows_ws blocks per XCD on MI355X (256 CUs)
+constexpr int SMFV_WS_BLOCKS_PER_XCD = 32;        // k_rows_ws blocks per XCD on MI355X (256 CUs), geometry 1
+constexpr int SMFV_WS_DEFAULT_GEOM = 1;           // (r4) k_rows_ws geometry without SMFV_PLAN_WS_GEOM1 / GEOM2
 constexpr int SMFV_WS_CHUNKED = 0;                // k_rows_ws tile order per block: 0 strided, 1 consecutive runs
 
 // The tile caps a plan with these flags uses for the row block whose first
@@ -1830,13 +1867,20 @@ constexpr int SMFV_WS_CHUNKED = 0;                // k_rows_ws tile order per bl
 static TileCaps plan_caps(int flags, int col_base)
 {
     TileCaps caps;
+    // (r4) the k_rows_ws geometry the tiles are cut for (WsGeom)
+    const int g = (flags & SMFV_PLAN_WS_GEOM2) ? 2 : (flags & SMFV_PLAN_WS_GEOM1) ? 1 : SMFV_WS_DEFAULT_GEOM;
+    caps.geom = g == 2 ? WS_GEOM2 : WS_GEOM1;
+    caps.ucap = caps.geom.ucap;
+    caps.ncap = caps.geom.ncap - 3 * caps.geom.rows();  // room for the quads' interleave padding
+    caps.maxrows = caps.geom.rows();
+    caps.xcd_blocks = caps.geom.xcd_blocks;
     caps.frontier = !(flags & SMFV_PLAN_NATURAL_SEEDS);
     caps.split_ends = (flags & SMFV_PLAN_SPLIT_ENDS) ? SMFV_WS_BLOCKS_PER_XCD : 0;
     caps.col_base = col_base;  // a row block's neighbours are its columns shifted by its first global row
 #ifdef SMFV_LAB
     // lab: smaller tiles (rows / entries / union) to measure what a unit costs
-    if (const char *e = std::getenv("SMFV_WS_MAXROWS")) caps.maxrows = std::max(8, std::min(WS_ROWS, atoi(e)));
-    if (const char *e = std::getenv("SMFV_WS_UCAP")) caps.ucap = std::max(8, std::min(WS_UCAP, atoi(e)));
+    if (const char *e = std::getenv("SMFV_WS_MAXROWS")) caps.maxrows = std::max(8, std::min(caps.maxrows, atoi(e)));
+    if (const char *e = std::getenv("SMFV_WS_UCAP")) caps.ucap = std::max(8, std::min(caps.ucap, atoi(e)));
 #endif
     return caps;
 }
@@ -1878,6 +1922,7 @@ struct smfv_plan_s {
     int64_t snapshot = 0;                  // values gathered by bind (tile entries + slack + direct rows)
     double reuse = 0.0, est_reuse = -1.0, analysis_ms = 0.0;
     int ws_xcd[9] = {};            // XCD x runs tiles [ws_xcd[x], ws_xcd[x + 1])
+    int ws_geom = 0;               // (r4) k_rows_ws geometry: 1 (WS_GEOM1) or 2 (WS_GEOM2)
     int parts = 1;                 // 8: one part of the rows per XCD (build_ws_plan)
     double footprint = -1.0;       // parts_footprint of the 8 parts
     int *tsrc = nullptr;                   // snapshot entry -> CSR index of its value (-1: pad)
@@ -2071,10 +2116,10 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
         if (!rc && go && !p->mfma && !p->cs && !(flags & SMFV_PLAN_MFMA)) {
             WsPlan W;
             std::string err;
-            if (!build_ws_plan(m, n, rpl.data(), cil, W, &err, caps)) {
-                set_error("%s", err.c_str());
-                rc = SMFV_ERR_INVALID;
-            } else {
+            // a pattern the tile layout cannot take (the replayed plan fails its
+            // checks) keeps the untiled plan rather than failing the create
+            if (build_ws_plan(m, n, rpl.data(), cil, W, &err, caps)) {
+                p->ws_geom = W.geom.cw == 4 ? 2 : 1;
                 p->ntiles = W.ntiles;
                 for (int x = 0; x <= 8; ++x) p->ws_xcd[x] = W.xcd[x];
                 p->parts = caps.part_start.size() > 2 ? (int)caps.part_start.size() - 1 : 1;
@@ -2394,6 +2439,7 @@ SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS])
     out[12] = plan->footprint;
     out[13] = !plan->tiled ? 0.0 : plan->cs ? 4.0 : plan->k1 ? 3.0 : plan->mfma ? 2.0 : 1.0;
     out[14] = plan->cs_chunks;
+    out[15] = plan->tiled && !plan->cs && !plan->k1 && !plan->mfma ? plan->ws_geom : 0;
     return SMFV_OK;
 }
 
@@ -2477,8 +2523,10 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             SMFV_LAUNCHED();
         }
     } else if (plan->ntiles > 0) {
-        // one persistent block per CU; a multiple of 8 (>= 8) so every XCD's tile range has blocks
-        const int blocks = std::max(8, (std::min(plan->ntiles, ncu) + 7) & ~7);
+        // persistent blocks: one (geometry 1) or two (geometry 2) per CU; a
+        // multiple of 8 (>= 8) so every XCD's tile range has blocks
+        const int per_cu = plan->ws_geom == 2 ? 2 : 1;
+        const int blocks = std::max(8, (std::min(plan->ntiles, per_cu * ncu) + 7) & ~7);
         int chunked = SMFV_WS_CHUNKED;
         // scalar-base addressing when X (n rows of ldx doubles) and the
         // snapshot each span < 4 GiB
@@ -2498,16 +2546,17 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             return e ? std::atoi(e) : -1;
         }();
         if (lab_chunked >= 0) chunked = lab_chunked;
-        auto kern = plan->fma ? (abl == 2 ? k_rows_ws_lab<2, true> : k_rows_ws<true>)
+        auto kern = plan->fma ? (abl == 2 ? k_rows_ws_lab<2, true> : WS1<true, true>)
                   : abl == 1 ? k_rows_ws_lab<1> : abl == 2 ? k_rows_ws_lab<2> : abl == 3 ? k_rows_ws_lab<3>
                   : abl == 4 ? k_rows_ws_lab<4> : abl == 5 ? k_rows_ws_lab<5> : abl == 6 ? k_rows_ws_lab<6>
                   : abl == 7 ? k_rows_ws_lab<7> : abl == 8 ? k_rows_ws_lab<8> : abl == 12 ? k_rows_ws_lab<12>
                   : abl == 13 ? k_rows_ws_lab<13> : abl == 14 ? k_rows_ws_lab<14> : abl == 15 ? k_rows_ws_lab<15> : abl == 16 ? k_rows_ws_lab<16>
-                  : abl == 9 ? (K == TILE_KP ? k_rows_ws_lab<9> : k_rows_ws<>)
-                  : abl == 10 ? (K == TILE_KP ? k_rows_ws_lab<10> : k_rows_ws<>)
-                  : abl == 11 ? (K == TILE_KP ? k_rows_ws_lab<11> : k_rows_ws<>)
-                  : abl == 17 ? (K == TILE_KP && plan->m >= 120000 ? k_rows_ws_lab<17> : k_rows_ws<>) : k_rows_ws<>;
-        if (!(saddr && lab_saddr)) kern = plan->fma ? k_rows_ws<true, false> : k_rows_ws<false, false>;
+                  : abl == 9 ? (K == TILE_KP ? k_rows_ws_lab<9> : WS1<false, true>)
+                  : abl == 10 ? (K == TILE_KP ? k_rows_ws_lab<10> : WS1<false, true>)
+                  : abl == 11 ? (K == TILE_KP ? k_rows_ws_lab<11> : WS1<false, true>)
+                  : abl == 17 ? (K == TILE_KP && plan->m >= 120000 ? k_rows_ws_lab<17> : WS1<false, true>) : WS1<false, true>;
+        // the lab's ablation copies are geometry 1 only
+        if (!(saddr && lab_saddr) || plan->ws_geom == 2) kern = pick_ws(plan->ws_geom, plan->fma, saddr && lab_saddr);
         static unsigned long long *stamp_buf = nullptr;
         const size_t stamp_n = (size_t)blocks * 16 * WS_STAMP_UNITS * 2;
         if (abl == 8 && !stamp_buf) {
@@ -2517,12 +2566,12 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         SMFV_REQUIRE(abl != 8 || blocks <= 256, "lab stamps: at most 256 blocks");
         if (abl == 8) SMFV_HIP(hipMemsetAsync(stamp_buf, 0, stamp_n * 8, st));
 #else
-        auto kern = saddr ? (plan->fma ? k_rows_ws<true> : k_rows_ws<>)
-                          : (plan->fma ? k_rows_ws<true, false> : k_rows_ws<false, false>);
+        auto kern = pick_ws(plan->ws_geom, plan->fma, saddr);
 #endif
         WsXcd xr;
         for (int x = 0; x <= 8; ++x) xr.first[x] = plan->ws_xcd[x];
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, st, xr, K / TILE_KP, chunked,
+        const int threads = plan->ws_geom == 2 ? WS_GEOM2.threads() : WS_GEOM1.threads();
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3((unsigned)threads), 0, st, xr, K / TILE_KP, chunked,
                            plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();
 #ifdef SMFV_LAB

@@ -40,19 +40,23 @@ struct ColumnRows {
         const int nc = std::max(n, 1);
         ptr.assign((size_t)nc + 1, 0);
         dptr.assign((size_t)nc + 1, 0);
+        // a row is listed once per column in `dist` even when its repeats of
+        // the column are not adjacent (unsorted rows): last row stamp per column
+        std::vector<int> last((size_t)nc, -1);
         for (int r = 0; r < m; ++r)
             for (int j = rp[r]; j < rp[r + 1]; ++j) {
                 ++ptr[(size_t)ci[j] + 1];
-                if (j == rp[r] || ci[j] != ci[j - 1]) ++dptr[(size_t)ci[j] + 1];  // rows are column-sorted
+                if (last[(size_t)ci[j]] != r) last[(size_t)ci[j]] = r, ++dptr[(size_t)ci[j] + 1];
             }
         for (int c = 0; c < nc; ++c) ptr[c + 1] += ptr[c], dptr[c + 1] += dptr[c];
         all.resize((size_t)ptr[(size_t)nc]);
         dist.resize((size_t)dptr[(size_t)nc]);
         std::vector<int64_t> fa(ptr.begin(), ptr.end() - 1), fd(dptr.begin(), dptr.end() - 1);
+        std::fill(last.begin(), last.end(), -1);
         for (int r = 0; r < m; ++r)
             for (int j = rp[r]; j < rp[r + 1]; ++j) {
                 all[(size_t)fa[(size_t)ci[j]]++] = r;
-                if (j == rp[r] || ci[j] != ci[j - 1]) dist[(size_t)fd[(size_t)ci[j]]++] = r;
+                if (last[(size_t)ci[j]] != r) last[(size_t)ci[j]] = r, dist[(size_t)fd[(size_t)ci[j]]++] = r;
             }
     }
 };
@@ -350,6 +354,8 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
         if (err) *err = "ws plan: " + msg;
         return false;
     };
+    const WsGeom G = P.geom;
+    const int R = G.rows();
     std::vector<char> seen((size_t)std::max(m, 1), 0);
     for (int r : P.direct) {
         if (r < 0 || r >= m || seen[r]) return fail("direct row out of range or repeated");
@@ -366,11 +372,11 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
             if (g[WS_G_NOFF + q] != noff || g[WS_G_TN + q] != tn || g[WS_G_NU + q] != nu ||
                 g[WS_G_VOFF + q] != voff || g[WS_G_TNV + q] != tnv)
                 return fail("record header not replicated");
-        if (noff % 32 || tn % 32 || tn <= 0 || tn > WS_NCAP || nu < 0 || nu > WS_UCAP ||
+        if (noff % 32 || tn % 32 || tn <= 0 || tn > G.ncap || nu < 0 || nu > G.ucap ||
             (int64_t)noff + tn > P.entries || voff % 8 || tnv % 8 || tnv < 0 || tnv > tn ||
             (int64_t)voff + tnv > P.ventries)
             return fail("tile header out of range");
-        for (int slot = 0; slot < WS_ROWS; ++slot) {
+        for (int slot = 0; slot < R; ++slot) {
             const int r = l[slot];
             if (r == -1) continue;
             if (r < 0 || r >= m || seen[r]) return fail("tile row out of range or repeated");
@@ -390,13 +396,13 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
         for (int q = 0; q < 256; ++q)
             if (g[q] < 0 || g[q] >= n) return "union id out of range";
         for (int e = noff; e < noff + tn; ++e)
-            if (P.loff[e] != WS_UCAP && P.loff[e] >= nu)
+            if (P.loff[e] != G.ucap && P.loff[e] >= nu)
                 return "entry offset outside the tile's union";
-        for (int slot = 0; slot < WS_ROWS; ++slot) {
+        for (int slot = 0; slot < R; ++slot) {
             const int r = l[slot];
             if (r == -1) continue;
-            const int lb = l[64 + slot] & 0xFFFF, len = l[64 + slot] >> 16, vb = l[128 + slot];
-            const int k = (slot >> 3) & 3;
+            const int lb = l[R + slot] & 0xFFFF, len = l[R + slot] >> 16, vb = l[2 * R + slot];
+            const int k = (slot / G.cw) & 3;  // the team's position in its quad
             const int rl = rp[r + 1] - rp[r];
             if (len % 2 || len < rl || len > rl + 1) return "row segment length";
             // the entries the kernel sums (len: the row's, rounded up to even);
@@ -409,17 +415,17 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
                     const int64_t ve = (int64_t)voff + (int64_t)(vb + 4 * (4 * b + u / 2) + k) * 2 + u % 2;
                     if (le >= noff + tn) return "segment leaves its tile";
                     if (el >= len) {  // never summed: the offset only has to stay on the zero row
-                        if (P.loff[le] != WS_UCAP) return "prefetched pad offset not on the zero row";
+                        if (P.loff[le] != G.ucap) return "prefetched pad offset not on the zero row";
                         continue;
                     }
                     if (ve >= voff + tnv) return "segment leaves its tile";
                     if (el < rl) {
                         const int j = rp[r] + el;
                         const int u_ = P.loff[le];
-                        const int w = (u_ / 4) % 8, i = (u_ / 4) / 8, qq = u_ % 4;
-                        if (P.tsrc[ve] != j || P.loff[le] == WS_UCAP || u_ >= nu || g[32 * w + 8 * qq + i] != ci[j])
+                        const int w = (u_ / 4) % G.lw, i = (u_ / 4) / G.lw, qq = u_ % 4;
+                        if (P.tsrc[ve] != j || P.loff[le] == G.ucap || u_ >= nu || g[32 * w + 8 * qq + i] != ci[j])
                             return "row entry is not its CSR non-zero";
-                    } else if (P.tsrc[ve] != -1 || P.loff[le] != WS_UCAP) {
+                    } else if (P.tsrc[ve] != -1 || P.loff[le] != G.ucap) {
                         return "pad entry does not read the zero row";
                     }
                 }
@@ -518,8 +524,14 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         t = now;
     };
     P = WsPlan();
+    const WsGeom G = caps.geom;
+    P.geom = G;
+    if (G.cw != 8 && G.cw != 4) {
+        if (err) *err = "ws plan: unsupported geometry";
+        return false;
+    }
     TileAnalysis T;
-    analyse_tiles(m, n, rp, ci, T, caps);  // TileCaps defaults are the k_rows_ws caps
+    analyse_tiles(m, n, rp, ci, T, caps);  // caps.ucap / ncap / maxrows follow caps.geom (plan_caps)
     tick("analyse_tiles");
 
     auto len8 = [&](int r) { return std::max(8, (rp[r + 1] - rp[r] + 7) & ~7); };
@@ -580,14 +592,20 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         }
         int *lrec = &P.lrec[(size_t)t * WS_LWORDS];
         int *grec = &P.grec[(size_t)t * WS_GWORDS];
-        for (int s = 0; s < WS_ROWS; ++s) lrec[s] = -1;
+        const int NR = G.rows();
+        for (int s = 0; s < NR; ++s) lrec[s] = -1;
         int64_t e = 0, ev = 0;
         for (int q = 0; 4 * q < (int)R.size(); ++q) {
-            const int o = q / 2, w = o < 4 ? o : 11 - o, h = q % 2;  // octet o -> wave; SIMD s runs octets s and 7 - s
+            // 8 compute waves: octet o = quads 2o, 2o + 1 -> one wave, and SIMD s
+            // runs octets s and 7 - s (a long and a short one); 4 compute waves
+            // (geometry 2, tiles often of 24 rows): quad q -> wave q % 4, half
+            // q / 4, so a tile of fewer than 32 rows still keeps all 4 waves busy
+            const int o = q / 2;
+            const int w = G.cw == 8 ? (o < 4 ? o : 11 - o) : q % 4, h = G.cw == 8 ? q % 2 : q / 4;
             const int nb = len8(R[4 * q]) / 8;
             const int lbase = (int)(e / 8), vbase = (int)(ev / 2);
             for (int k = 0; k < 4 && 4 * q + k < (int)R.size(); ++k) {
-                const int r = R[4 * q + k], slot = (4 * h + k) * 8 + w;
+                const int r = R[4 * q + k], slot = (4 * h + k) * G.cw + w;
                 for (int j = rp[r]; j < rp[r + 1]; ++j) {
                     const int el = j - rp[r];
                     P.loff[(size_t)(noff + (int64_t)(lbase + 4 * (el / 8) + k) * 8 + el % 8)] =
@@ -595,17 +613,17 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
                     P.tsrc[(size_t)(vnoff + (int64_t)(vbase + 4 * (el / 2) + k) * 2 + el % 2)] = j;
                 }
                 lrec[slot] = r;
-                lrec[64 + slot] = lbase | (len2(r) << 16);
-                lrec[128 + slot] = vbase;
+                lrec[NR + slot] = lbase | (len2(r) << 16);
+                lrec[2 * NR + slot] = vbase;
                 tiled += rp[r + 1] - rp[r];
             }
             e += 32 * nb;
             ev += vquad(R, (size_t)(4 * q));
         }
-        for (int w = 0; w < WS_LOADERS; ++w)
+        for (int w = 0; w < G.lw; ++w)
             for (int q = 0; q < 4; ++q)
                 for (int i = 0; i < 8; ++i) {
-                    const int u = 4 * (w + 8 * i) + q;
+                    const int u = 4 * (w + G.lw * i) + q;
                     grec[32 * w + 8 * q + i] = u < nu ? ucols[u] : 0;
                 }
         for (int q = 0; q < 16; ++q) {
@@ -639,7 +657,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         }
         std::vector<int> sorted = rows;
         by_length(sorted);
-        if (layout(sorted) <= WS_NCAP) {
+        if (layout(sorted) <= G.ncap) {
             tiles.push_back(std::move(rows));
             continue;
         }
@@ -647,7 +665,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         while (!stack.empty()) {
             std::vector<int> R = std::move(stack.back());
             stack.pop_back();
-            if (layout(R) <= WS_NCAP) {
+            if (layout(R) <= G.ncap) {
                 tiles.push_back(std::move(R));
             } else if (R.size() == 1) {
                 P.direct.push_back(R[0]);
@@ -719,7 +737,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         if (err) *err = "ws plan: too many tile entries for int32 offsets";
         return false;
     }
-    P.loff.assign((size_t)(P.entries + WS_SLACK), (uint8_t)WS_UCAP);
+    P.loff.assign((size_t)(P.entries + WS_SLACK), (uint8_t)G.ucap);
     P.tsrc.assign((size_t)(P.ventries + WS_SLACK), -1);
     P.grec.assign((size_t)nt * WS_GWORDS, 0);
     P.lrec.assign((size_t)nt * WS_LWORDS, 0);

@@ -39,11 +39,28 @@ constexpr int WS_ZOFF = WS_UCAP * 256;  // byte offset of the zero row
 // entries; its union rows) and voff / tnv (its values: first entry, entries),
 // each replicated 16x so any lane reads its copy with no broadcast
 constexpr int WS_GWORDS = 352, WS_G_NOFF = 256, WS_G_TN = 272, WS_G_NU = 288, WS_G_VOFF = 304, WS_G_TNV = 320;
-// LDS record (per tile, 256 int32 = 1 KiB): [0, 64) row per team slot (-1 none),
-// [64, 128) L chunk base | (padded length << 16), [128, 192) V chunk base;
-// team slot = team-in-wave * 8 + wave
+// LDS record (per tile, 256 int32 = 1 KiB in global memory): with R rows per
+// tile, [0, R) row per team slot (-1 none), [R, 2R) L chunk base | (padded
+// length << 16), [2R, 3R) V chunk base; team slot = team-in-wave * (compute
+// waves) + wave
 constexpr int WS_LWORDS = 256;
 constexpr int WS_SLACK = 2048;   // entries past the end (DMA over-read of the last tile)
+
+// (r4) Geometry of a k_rows_ws launch.  cw compute waves of 8 eight-lane
+// teams (rows per tile = 8 cw), lw loader waves of 8 one-KiB X pieces each
+// (ucap + 1 <= 32 lw), entry cap ncap, xcd_blocks blocks per XCD.
+//   WS_GEOM1: one 1024-lane block per CU, 64-row tiles, 158 KiB of LDS.
+//   WS_GEOM2: two 512-lane blocks per CU, 32-row tiles, 80 KiB of LDS each:
+//             two independent two-slot pipelines per CU, so one block's
+//             per-unit hand-off (landing wait + barrier) hides behind the
+//             other block's work.
+struct WsGeom {
+    int cw, lw, ucap, ncap, xcd_blocks;
+    constexpr int rows() const { return 8 * cw; }
+    constexpr int threads() const { return 64 * (cw + lw); }
+};
+constexpr WsGeom WS_GEOM1{8, 8, WS_UCAP, WS_NCAP, 32};
+constexpr WsGeom WS_GEOM2{4, 4, 125, 896, 64};
 
 // Per-tile summary of the clustered analysis.
 struct TileMeta {
@@ -97,6 +114,7 @@ struct TileCaps {
     // parts runs part x on XCD x (range_parts / bfs_parts below)
     std::vector<int> part_rows, part_start;
     int xcd_blocks = 32;           // k_rows_ws blocks per XCD (MI355X: 256 CUs / 8 XCDs)
+    WsGeom geom = WS_GEOM1;        // build_ws_plan: the kernel geometry (ucap / ncap / maxrows follow it)
     int cs_rows = 0;               // build_cs_plan: rows per tile (0: the fewest rounds of <= CS_ROWS per block)
 };
 // Independent parts are analysed on up to 8 threads; analysis_threads > 0
@@ -106,6 +124,7 @@ void analyse_tiles(int m, int n, const int *row_ptr, const int *col_idx, TileAna
 extern thread_local int analysis_threads;
 
 struct WsPlan {
+    WsGeom geom = WS_GEOM1;
     int ntiles = 0;
     std::vector<int> grec;         // WS_GWORDS per tile
     std::vector<int> lrec;         // WS_LWORDS per tile

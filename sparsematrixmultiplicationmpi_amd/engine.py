@@ -117,7 +117,8 @@ def _check_dense(T: torch.Tensor, rows: int, K: int, name: str) -> int:
 
 PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA, PLAN_NATURAL_SEEDS, PLAN_MFMA, PLAN_SPLIT_ENDS = 1, 2, 4, 8, 16, 32
 PLAN_ONE_WAVEFRONT, PLAN_SIMPLE_ROWS, PLAN_CS, PLAN_WS = 64, 128, 256, 512
-PLAN_STATS = 15  # SMFV_PLAN_STATS
+PLAN_WS_GEOM1, PLAN_WS_GEOM2 = 1024, 2048
+PLAN_STATS = 16  # SMFV_PLAN_STATS
 PLAN_KERNELS = {0: None, 1: "k_rows_ws", 2: "k_rows_mfma", 3: "k_spmv_chunks", 4: "k_rows_cs"}
 
 
@@ -153,8 +154,11 @@ class SpmmPlan:
         if {"auto": False, "one": True}[xcd_parts]:
             flags |= PLAN_ONE_WAVEFRONT
         # which tiled kernel for K % 32 == 0: the library's choice, or k_rows_cs
-        # (column-streamed tiles, SMFV_PLAN_CS) / k_rows_ws (SMFV_PLAN_WS) for A/B
-        flags |= {"auto": 0, "cs": PLAN_CS, "ws": PLAN_WS}[tiled_kernel]
+        # (column-streamed tiles, SMFV_PLAN_CS) / k_rows_ws (SMFV_PLAN_WS) for
+        # A/B; "ws1" / "ws2": k_rows_ws with one 1024-lane / two 512-lane
+        # pipelines per CU (SMFV_PLAN_WS_GEOM1 / GEOM2)
+        flags |= {"auto": 0, "cs": PLAN_CS, "ws": PLAN_WS, "ws1": PLAN_WS | PLAN_WS_GEOM1,
+                  "ws2": PLAN_WS | PLAN_WS_GEOM2}[tiled_kernel]
         self._plan = ctypes.c_void_p()
         ip = ctypes.POINTER(ctypes.c_int)
         if rows is None:
@@ -180,7 +184,8 @@ class SpmmPlan:
                 "reuse": float(out[3]), "plan_bytes": int(out[4]), "direct_rows": int(out[5]),
                 "row_begin": int(out[6]), "est_reuse": float(out[7]), "analysis_ms": float(out[8]),
                 "snapshot_entries": int(out[9]), "mfma": bool(out[10]), "xcd_parts": int(out[11]),
-                "footprint": float(out[12]), "kernel": PLAN_KERNELS.get(int(out[13])), "chunks": int(out[14])}
+                "footprint": float(out[12]), "kernel": PLAN_KERNELS.get(int(out[13])), "chunks": int(out[14]),
+                "ws_geom": int(out[15])}
 
     def run(self, X: torch.Tensor, Y: torch.Tensor, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
         A, K = self.A, self.K
