@@ -746,6 +746,128 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     return None
 
 
+def bench_rank_plans(args, kind: str, K: int, variant: str) -> None:
+    """--rank-plans p: a ONE-GPU PROJECTION of the p-GPU decomposition, not a
+    scaling measurement.  Every rank r of p runs its share on this one device
+    through the product's own rank plan (smfv_dist_plan_create_rank: the same
+    partition -- SC/...RowWise.cpp:26-29, ...ColumnWise.cpp:25-28,
+    ...NonZeroElement.cpp:24-39 -- and the same single-device plan a rank of
+    smfv_dist_plan_create runs), timed alone like the headline (cold rotation
+    over copies, one hipGraph of `steps` launches).  Reports the rank-local
+    time per rank (max / min), its algorithmic bytes, and the bytes each rank
+    contributes to the exchange (RowWise / ColumnWise: its Y block or panel;
+    NonZeroElement: its compact partial rows), which the p-GPU step moves over
+    xGMI after the slowest rank.  After timing, every rank's share is
+    assembled as the exchange would (device copies) and checked against the
+    one-GPU untiled sequential plan."""
+    import numpy as np
+    import torch
+    import sparsematrixmultiplicationmpi_amd as smfv
+    from sparsematrixmultiplicationmpi_amd import dist as D
+    from sparsematrixmultiplicationmpi_amd import engine as S
+    from sparsematrixmultiplicationmpi_amd import inputs
+
+    p = args.rank_plans
+    A, label = build_matrix(kind, args.mtx)
+    m, n, nnz = A.numRows, A.numCols, A.nnz
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    V = smfv.Variant[variant]
+    X_host = inputs.generateLargeFatVector(n, K)
+    prob_bytes = algorithmic_bytes(m, n, nnz, K)
+    ncopies = max(1, min(16, math.ceil(args.cold_bytes / prob_bytes) + 1))
+    first, last, off, cnt = D.exchange_plan(V, m, nnz, A.rowPtr, K, p)
+    copies = []
+    for c in range(ncopies):
+        dA = smfv.DeviceCSR(A, dev)
+        dX = torch.from_numpy(X_host).to(dev)
+        dY = torch.zeros((m, K), dtype=torch.float64, device=dev)
+        plans = [D.DistPlan(None, V, dA, K, to_all=False, rank=(r, p), tiles=args.tiles,
+                            tiled_kernel=args.tiled_kernel) for r in range(p)]
+        copies.append((plans, dX, dY))
+    torch.cuda.synchronize()
+    ranks = []
+    for r in range(p):
+        def step(i, r=r):
+            plans, dX, dY = copies[i % ncopies]
+            plans[r].run_local(dX, dY)
+        for i in range(max(args.warmup, ncopies)):
+            step(i)
+        ms, how = _graph_or_eager(step, args.steps, 1)
+        st = copies[0][0][r].stats()
+        if V == smfv.Variant.ROWWISE:
+            r0, r1 = int(first[r]), int(last[r]) + 1
+            lb = 12 * (int(A.rowPtr[r1]) - int(A.rowPtr[r0])) + 4 * (r1 - r0 + 1) + \
+                8 * _x_rows_touched(A, r0, r1) * K + 8 * (r1 - r0) * K if r1 > r0 else 0
+        elif V == smfv.Variant.COLUMNWISE:
+            kc = int(last[r] - first[r] + 1)
+            lb = 12 * nnz + 4 * (m + 1) + 8 * n * kc + 8 * m * kc if kc > 0 else 0
+        else:
+            s_, e_ = _partition_nnz(nnz, p, r)
+            rows = int(last[r] - first[r] + 1) if e_ > s_ else 0
+            lb = 12 * (e_ - s_) + 8 * _x_rows_touched_nnz(A, s_, e_) * K + 8 * rows * K
+        ranks.append({"rank": r, "local_ms": round(ms, 6), "algorithmic_bytes": int(lb),
+                      "GBps": round(lb / (ms * 1e-3) / 1e9, 1) if ms > 0 else None,
+                      "exchange_bytes": int(cnt[r]) * 8, "tiled": st["tiled"], "tiles": st["tiles"],
+                      "ws_geom": st.get("ws_geom"), "timing": how})
+    # the shares assembled as the exchange would, against the 1-GPU sequential plan
+    plans, dX, dY = copies[0]
+    dY.fill_(float("nan"))
+    xbuf = None
+    if V != smfv.Variant.ROWWISE:
+        xbuf = torch.full((max(int((off + cnt).max()), 1),), float("nan"), dtype=torch.float64, device=dev)
+    for r in range(p):
+        plans[r].run_local(dX, dY)
+        b = plans[r].exchange_buffer()
+        if b is not None and cnt[r] > 0:
+            xbuf[int(off[r]):int(off[r] + cnt[r])] = b[int(off[r]):int(off[r] + cnt[r])]
+    if V == smfv.Variant.COLUMNWISE:
+        smfv._lib.call("smfv_panels_to_rowmajor_f64", m, K, p, xbuf.data_ptr(), dY.data_ptr(), K, S.stream_handle())
+    elif V == smfv.Variant.NONZERO:
+        import ctypes
+        rfa = (ctypes.c_int * p)(*[int(v) for v in first])
+        rla = (ctypes.c_int * p)(*[int(v) for v in last])
+        smfv._lib.call("smfv_combine_row_blocks_f64", m, K, p, rfa, rla, xbuf.data_ptr(), dY.data_ptr(), K,
+                       S.stream_handle())
+    ref = smfv.SpmmPlan(smfv.Variant.SEQUENTIAL, plans[0].A, K, tiles="off")
+    Yr = torch.empty_like(dY)
+    ref.run(dX, Yr)
+    mabs, _ = smfv.compare(Yr, dY)
+    ok = mabs == 0.0 if V != smfv.Variant.NONZERO else mabs <= 1e-6
+    loc = [x["local_ms"] for x in ranks]
+    flops = 2.0 * nnz * K
+    xbytes = [x["exchange_bytes"] for x in ranks]
+    print(json.dumps({
+        "projection": f"{p}-GPU decomposition projected on ONE GPU (each rank's share timed alone, in turn); "
+                      "not a scaling measurement: no RCCL, no concurrent ranks",
+        "metric": metric_for(args.config, K, variant), "unit": "us", "config": args.config, "variant": variant,
+        "p": p, "steps": args.steps, "copies_rotated": ncopies,
+        "rank_local_us_max": round(max(loc) * 1e3, 3), "rank_local_us_min": round(min(loc) * 1e3, 3),
+        "ideal_us_1_over_p_of_1gpu": None,
+        "projected_GFLOPs_without_exchange": round(flops / (max(loc) * 1e-3) / 1e9, 1),
+        "exchange_bytes_max": max(xbytes), "exchange_bytes_total": int(sum(xbytes)),
+        "exchange_note": "bytes a rank's block adds to the exchange (TO_ALL: every rank receives all others' "
+                         "blocks: the all-gather moves (p-1)/p of the total into each GPU)",
+        "ranks": ranks, "tiled_kernel": args.tiled_kernel,
+        "check": {"ok": bool(ok), "max_abs_diff": mabs,
+                  "criterion": "shares assembled as the exchange would vs the 1-GPU untiled sequential plan "
+                               "(bit-identical; NONZERO 1e-6)"}}))
+    if not ok and not args.no_check:
+        sys.exit(3)
+
+
+def _partition_nnz(nnz: int, p: int, r: int):
+    """Rank r's nnz range [s, e) of SC/...NonZeroElement.cpp:24-39 (smfv_partition_nnz)."""
+    q, extra = divmod(nnz, p)
+    s = r * (q + 1) if r < extra else r * q + extra
+    return s, s + q + (1 if r < extra else 0)
+
+
+def _x_rows_touched_nnz(A, s: int, e: int) -> int:
+    import numpy as np
+    return int(np.unique(np.asarray(A.colIndices[s:e])).size) if e > s else 0
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -780,12 +902,16 @@ def main() -> None:
                     help="report the post-timing result check but do not fail on it (lab ablations)")
     ap.add_argument("--mfma", action="store_true",
                     help="time the opt-in dense-block MFMA tile kernel (SMFV_PLAN_MFMA, config 3's MFMA K-panel)")
-    ap.add_argument("--tiled-kernel", default="auto", choices=["auto", "cs", "ws", "ws1", "ws2"],
+    ap.add_argument("--tiled-kernel", default="auto", choices=["auto", "cs", "ws", "ws1", "ws2", "ws3"],
                     help="tiled kernel for K % 32 == 0: the library's choice, k_rows_cs (SMFV_PLAN_CS) "
                          "or k_rows_ws (SMFV_PLAN_WS), A/B; ws1 / ws2: k_rows_ws with one 1024-lane / two 512-lane "
                          "pipelines per CU (SMFV_PLAN_WS_GEOM1 / GEOM2)")
     ap.add_argument("--fma", action="store_true",
                     help="time the opt-in FMA plans (SMFV_PLAN_FMA) instead of the bit-exact ones")
+    ap.add_argument("--rank-plans", type=int, default=0,
+                    help="p > 0: a one-GPU projection of the p-rank decomposition -- every rank's share timed in "
+                         "turn through its rank plan (smfv_dist_plan_create_rank); prints a projection line, not "
+                         "the headline")
     ap.add_argument("--phase-timeout", type=float, default=240.0,
                     help="multi-GPU paths: seconds a phase (RCCL set-up, plans, warm-up, timing, check) may take "
                          "before a diagnostic JSON line and exit status 4 (0 = no watchdog)")
@@ -798,6 +924,9 @@ def main() -> None:
     variant = args.variant or variant
     if kind == "syn80m":
         bench_rowpart(args, world, rank, local, K)
+        return
+    if args.rank_plans > 0:
+        bench_rank_plans(args, kind, K, variant)
         return
     mode = args.mode or ("decomposed" if world > 1 else "replicas")
     fallback = None

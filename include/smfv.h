@@ -179,11 +179,11 @@ typedef struct smfv_plan_s *smfv_plan_t;
  * variants are checked against (SC/main.cpp:184) -- so that check does not
  * compare a kernel with itself.  Ignored for SMFV_NONZERO. */
 #define SMFV_PLAN_SIMPLE_ROWS 128
-/* Column-streamed tiles (k_rows_cs, K % 32 == 0): two tiles of ~m / 512 rows
- * per CU, each row's 32 panel columns held in registers for the whole tile,
- * the tile's X rows streamed through LDS in column-sorted chunks; each row is
- * still summed in CSR order (bit-identical).  Needs column-sorted CSR rows
- * (otherwise the plan keeps k_rows_ws). */
+/* LAB BUILD ONLY (libsmfv_lab.so; since r4 libsmfv.so ignores the flag and
+ * keeps k_rows_ws): column-streamed tiles (k_rows_cs, K % 32 == 0), two
+ * tiles of ~m / 512 rows per CU, each row's 32 panel columns held in
+ * registers, the tile's X rows streamed through LDS in column-sorted chunks;
+ * bit-identical, measured 3.4x slower than k_rows_ws. */
 #define SMFV_PLAN_CS 256
 /* The former tiled kernel (k_rows_ws: ~60-row tiles whose whole X union sits
  * in LDS) where SMFV_PLAN_CS would be the default (A/B). */
@@ -196,6 +196,10 @@ typedef struct smfv_plan_s *smfv_plan_t;
  * behind the other's work.  Same per-row order: bit-identical either way. */
 #define SMFV_PLAN_WS_GEOM1 1024
 #define SMFV_PLAN_WS_GEOM2 2048
+/* (r4) GEOM3: one 768-lane block per CU, 8 compute + 4 loader waves (16 X
+ * pieces each), 64-row tiles: 3 waves per SIMD, so the compute waves may hold
+ * up to 168 VGPRs (deeper LDS read-ahead). */
+#define SMFV_PLAN_WS_GEOM3 4096
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
 /* Plan of the row block [row_begin, row_end) of a CSR matrix (h_row_ptr /
@@ -234,15 +238,6 @@ SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int
  * mean fill of a chunk's slots, [5] 1 for the wide layout (32-bit columns:
  * some row spans more than 65,535 columns), 0 for 16-bit offsets.  No device
  * needed.  (SC/SparseMatrixFatVectorMultiply.cpp:17-27 at vecCols = 1.) */
-/* The column-streamed tile plan (k_rows_cs, SMFV_PLAN_CS) of the row block
- * [row_begin, row_end), built and verified as smfv_plan_create_rows builds it
- * (rows_per_tile 0: the plan's own choice, else 1..256): out[0] tiles,
- * [1] chunks, [2] staged X rows per panel, [3] re-use, [4] value slots incl.
- * pads, [5] non-zeros, [6] chunks of the busiest block of the 8 x 32 grid,
- * [7] steps of the busiest SIMD summed over the busiest block's chunks.
- * No device needed. */
-SMFV_API int smfv_cs_plan_analyse(int row_begin, int row_end, int n, const int *h_row_ptr,
-                                  const int *h_col_idx, int flags, int rows_per_tile, double out[8]);
 SMFV_API int smfv_spmv_chunks_analyse(int row_begin, int row_end, int n, const int *h_row_ptr,
                                       const int *h_col_idx, int cap, double out[6]);
 SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int *d_col_idx,
@@ -258,7 +253,8 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
  * over the pattern's X rows (-1: not computed), [13] the kernel a tiled
  * plan runs: 0 none (untiled), 1 k_rows_ws, 2 k_rows_mfma, 3 k_spmv_chunks,
  * 4 k_rows_cs; [14] chunks of a k_rows_cs plan; [15] (r4) the k_rows_ws
- * geometry (1: one 1024-lane block per CU, 2: two 512-lane blocks; 0 other) */
+ * geometry (1: one 1024-lane block per CU, 2: two 512-lane blocks, 3: one
+ * 768-lane block; 0 other) */
 #define SMFV_PLAN_STATS 16
 SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS]);
 SMFV_API int smfv_plan_destroy(smfv_plan_t plan);

@@ -57,7 +57,6 @@ _SIGS = {
     "smfv_plan_analyse": (c_int, [c_int, c_int, _PI, _PI, _PD]),
     "smfv_plan_analyse_rows": (c_int, [c_int, c_int, c_int, _PI, _PI, c_int, _PD]),
     "smfv_spmv_chunks_analyse": (c_int, [c_int, c_int, c_int, _PI, _PI, c_int, _PD]),
-    "smfv_cs_plan_analyse": (c_int, [c_int, c_int, c_int, _PI, _PI, c_int, c_int, _PD]),
     "smfv_set_analysis_threads": (None, [c_int]),
     "smfv_plan_bind_values": (c_int, [c_void_p, c_void_p, c_void_p]),
     "smfv_plan_execute": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
@@ -137,6 +136,14 @@ _SIGS = {
 }
 
 
+# lab build only (libsmfv_lab.so): the column-streamed tile plan's analysis
+# (csrc/lab/cs_plan_lab.h), out of the product since r4
+_LAB_SIGS = {
+    "smfv_cs_plan_analyse": (c_int, [c_int, c_int, c_int, _PI, _PI, c_int, c_int, _PD]),
+}
+LAB = LIB_PATH.endswith("libsmfv_lab.so")
+
+
 def _load() -> ctypes.CDLL:
     # torch bundles its own ROCm runtime (libamdhip64.so.7, librccl.so.1,
     # libhsa-runtime64.so.1).  Importing it FIRST makes libsmfv.so's NEEDED
@@ -149,7 +156,7 @@ def _load() -> ctypes.CDLL:
             f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
             "(make -C sparsematrixmultiplicationmpi_amd/csrc). There is no CPU fallback.")
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
-    for name, (res, args) in _SIGS.items():
+    for name, (res, args) in (dict(_SIGS, **_LAB_SIGS) if LAB else _SIGS).items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

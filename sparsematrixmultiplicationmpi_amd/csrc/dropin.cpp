@@ -599,6 +599,7 @@ struct PlanEntry {
     Plans tiled;                    // the background build's result, once taken
     std::future<Plans> building;    // the background build (valid until taken)
     bool build_pending = false;     // to be started when the current call has returned its result
+    int calls = 0;                  // calls that used this entry (world > 1: the tiled build is on call 2)
     int world = 1, device = 0;
     bool tiled_ready = false;
     uint64_t used = 0;
@@ -692,7 +693,13 @@ PlanEntry &plan_for(int variant, const Problem &P, int world)
         if (!ne->untiled.local && !ne->untiled.dist) check(SMFV_ERR_INVALID, "smfv plan create (untiled)");
         const bool may_tile = variant != SMFV_SEQUENTIAL && P.K % 32 == 0 && P.m > 0 && P.nnz > 0;
         if (may_tile) {
-            ne->build_pending = true;  // started by start_pending_builds() once this call is done
+            // world 1: built in the background, started by start_pending_builds()
+            // once this call is done.  world > 1: no background
+            // thread allocating device memory while this rank's RCCL exchanges
+            // run; the tiled distributed plan is built on the calling thread at
+            // the pattern's second call, the same call on every rank (the
+            // calls are collective), so the ranks switch plans together
+            ne->build_pending = world == 1;
             ne->world = world;
             ne->device = dev;
         } else {
@@ -702,6 +709,12 @@ PlanEntry &plan_for(int variant, const Problem &P, int world)
         e = v.back().get();
     }
     e->used = ++tick;
+    if (++e->calls == 2 && world > 1 && !e->tiled_ready) {
+        e->tiled = create_plans(e->key.variant, e->key.m, e->key.n, e->key.nnz, e->rp->data(), e->ci->data(),
+                                e->key.K, world, 0, e->device);
+        e->tiled_ready = true;
+        if (!e->tiled.tiled()) e->tiled.destroy();
+    }
     if (!e->tiled_ready && e->building.valid() &&
         e->building.wait_for(std::chrono::seconds(0)) == std::future_status::ready) {
         e->tiled = e->building.get();
@@ -723,10 +736,17 @@ void start_pending_builds()
         static const bool registered = std::atexit(join_background_builds) == 0;
         (void)registered;
         raw->building = std::async(std::launch::async, [raw]() {
-            setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), 10);  // behind the caller's own work
-            smfv_set_analysis_threads(4);
-            return create_plans(raw->key.variant, raw->key.m, raw->key.n, raw->key.nnz, raw->rp->data(),
-                                raw->ci->data(), raw->key.K, raw->world, 0, raw->device);
+            // never throws: an exception here would be rethrown by get() in a
+            // destructor or the atexit join (std::terminate); an empty Plans
+            // keeps the untiled plan
+            try {
+                setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), 10);  // behind the caller's own work
+                smfv_set_analysis_threads(4);
+                return create_plans(raw->key.variant, raw->key.m, raw->key.n, raw->key.nnz, raw->rp->data(),
+                                    raw->ci->data(), raw->key.K, raw->world, 0, raw->device);
+            } catch (...) {
+                return Plans();
+            }
         });
     }
 }

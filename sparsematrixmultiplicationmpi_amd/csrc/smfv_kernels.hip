@@ -45,6 +45,9 @@
 
 #include "smfv_internal.h"
 #include "smfv_plan.h"
+#ifdef SMFV_LAB
+#include "lab/cs_plan_lab.h"  // k_rows_cs plan (lab only)
+#endif
 
 #pragma clang fp contract(off)
 
@@ -511,7 +514,7 @@ namespace ws {
 constexpr int XSLOT = (WS_UCAP + 1) * 256;  // X image: union rows + the zero row, 256 B each
 constexpr int SL_M = 2 * XSLOT;             // meta slots follow the X slots
 // values and offsets arrive in whole 1 KiB DMA pieces (128 doubles / 1,024 u8)
-constexpr int M_V = 0, M_L = (WS_NCAP + 127) / 128 * 1024, M_R = M_L + (WS_NCAP + 1023) / 1024 * 1024,
+[[maybe_unused]] constexpr int M_V = 0, M_L = (WS_NCAP + 127) / 128 * 1024, M_R = M_L + (WS_NCAP + 1023) / 1024 * 1024,
               MSLOT = M_R + WS_LWORDS * 4;
 static_assert(SL_M + 2 * MSLOT <= 160 * 1024, "two X and two meta slots must fit the CU's 160 KiB");
 static_assert(XSLOT % 1024 == 0 && MSLOT % 1024 == 0, "1 KiB DMA pieces");
@@ -561,7 +564,7 @@ __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(
 // images of UCAP + 1 rows (the last one zero), then two meta slots of values,
 // u8 offsets and the tile's record ([0, R) rows, [R, 2R) L bases, [2R, 3R) V
 // bases; 1 KiB for 64-row tiles, 384 B rounded to 512 for 32-row tiles)
-template <int CW, int LW, int UCAP, int NCAP> struct Lay {
+template <int CW, int LW, int PPW, int UCAP, int NCAP> struct Lay {
     static constexpr int R = 8 * CW;
     static constexpr int XSLOT = (UCAP + 1) * 256;
     static constexpr int SL_M = 2 * XSLOT;
@@ -572,7 +575,7 @@ template <int CW, int LW, int UCAP, int NCAP> struct Lay {
     static constexpr int BYTES = SL_M + 2 * MSLOT;
     static constexpr int ZOFF = UCAP * 256;
     static_assert(BYTES <= (CW == 8 ? 160 : 80) * 1024, "the blocks of one CU share its 160 KiB");
-    static_assert(UCAP + 1 <= 4 * 8 * LW, "8 X pieces per loader wave cover the image");
+    static_assert(UCAP + 1 <= 4 * PPW * LW && PPW % 4 == 0, "PPW X pieces per loader wave cover the image");
     static_assert(UCAP <= 255, "u8 image offsets");
     static_assert(XSLOT % 16 == 0 && MSLOT % 16 == 0 && M_L % 1024 == 0, "16-byte DMA lanes");
 };
@@ -583,7 +586,7 @@ template <int CW, int LW, int UCAP, int NCAP> struct Lay {
 struct WsXcd {
     int first[9];  // XCD x runs tiles [first[x], first[x + 1]) of the plan's order
 };
-template <int CW, int LW, int UCAP, int NCAP, bool FMA = false, bool SADDR = true>
+template <int CW, int LW, int PPW, int UCAP, int NCAP, bool FMA = false, bool SADDR = true>
 __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsXcd xr, int npanel, int chunked,
                                                      const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
@@ -593,7 +596,7 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
                                                      double *__restrict__ Y, int64_t ldy)
 {
     using namespace ws;
-    using L = Lay<CW, LW, UCAP, NCAP>;
+    using L = Lay<CW, LW, PPW, UCAP, NCAP>;
     constexpr int XSLOT = L::XSLOT, SL_M = L::SL_M, M_V = L::M_V, M_L = L::M_L, M_R = L::M_R, MSLOT = L::MSLOT;
     __shared__ __attribute__((aligned(16))) char lds[L::BYTES];
     int t0, tstep, cnt;
@@ -631,15 +634,15 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
         const int wl = wv - CW;
         if (wl == 0 && lane < 32)  // zero row of both X slots
             reinterpret_cast<d2 *>(lds + (lane >> 4) * XSLOT + L::ZOFF)[lane & 15] = d2{0.0, 0.0};
-        i4 u0, u1;
+        i4 ur[PPW / 4];                       // union ids of this lane's pieces
         int noff, tn, nu, voff, tnv;
-        unsigned xo[8];                       // SADDR: byte offset of this lane's 16 B of union row uc[i]
+        unsigned xo[PPW];                     // SADDR: byte offset of this lane's 16 B of union row uc[i]
         const unsigned ldxb = (unsigned)(ldx * 8);
         auto fetch_record = [&](int t) {
             const int *G = grec + (int64_t)t * WS_GWORDS;
-            const i4 *gu = reinterpret_cast<const i4 *>(G + 32 * wl + 8 * (lane >> 4));
-            u0 = gu[0];
-            u1 = gu[1];
+            const i4 *gu = reinterpret_cast<const i4 *>(G + 4 * PPW * wl + PPW * (lane >> 4));
+#pragma unroll
+            for (int k = 0; k < PPW / 4; ++k) ur[k] = gu[k];
             noff = G[WS_G_NOFF + (lane & 15)];
             tn = G[WS_G_TN + (lane & 15)];
             nu = G[WS_G_NU + (lane & 15)];
@@ -650,14 +653,19 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
         auto stage = [&](int t, int p, int xs, int ms) {
             // hipcc does not count the asm DMAs: resolve the record registers
             // here, so no wait it places for them lands between two DMAs
-            asm volatile("" ::"v"(u0), "v"(u1), "v"(noff), "v"(tn), "v"(nu), "v"(voff), "v"(tnv));
+#pragma unroll
+            for (int k = 0; k < PPW / 4; ++k) asm volatile("" ::"v"(ur[k]));
+            asm volatile("" ::"v"(noff), "v"(tn), "v"(nu), "v"(voff), "v"(tnv));
             const unsigned xb = lds0 + xs * XSLOT;
-            const int uc[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+            int uc[PPW];
+#pragma unroll
+            for (int k = 0; k < PPW / 4; ++k)
+                uc[4 * k] = ur[k].x, uc[4 * k + 1] = ur[k].y, uc[4 * k + 2] = ur[k].z, uc[4 * k + 3] = ur[k].w;
             const int cp = p * TILE_KP;
             if constexpr (SADDR)
                 if (p == 0)  // per tile: the union rows' byte offsets (panels add to the scalar base)
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) xo[i] = (unsigned)uc[i] * ldxb + 16u * (unsigned)(lane & 15);
+                    for (int i = 0; i < PPW; ++i) xo[i] = (unsigned)uc[i] * ldxb + 16u * (unsigned)(lane & 15);
             auto stage_meta = [&]() {
                 const unsigned mb = lds0 + SL_M + ms * MSLOT;
                 if constexpr (SADDR) {
@@ -680,7 +688,7 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
                 }
             };
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
+            for (int i = 0; i < PPW; ++i) {
                 const int piece = wl + LW * i;  // 1 KiB = union rows 4*piece .. +3 (pieces dealt round-robin)
                 const int u = 4 * piece + (lane >> 4);
                 if (4 * piece < nu && u < UCAP) {
@@ -849,254 +857,23 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
 #endif
 
 // the product instances of k_rows_ws: geometry (smfv_plan.h WsGeom) x FMA x SADDR
-template <bool FMA, bool SADDR>
-constexpr auto WS1 = k_rows_ws<WS_GEOM1.cw, WS_GEOM1.lw, WS_GEOM1.ucap, WS_GEOM1.ncap, FMA, SADDR>;
-template <bool FMA, bool SADDR>
-constexpr auto WS2 = k_rows_ws<WS_GEOM2.cw, WS_GEOM2.lw, WS_GEOM2.ucap, WS_GEOM2.ncap, FMA, SADDR>;
+#define SMFV_WS_INST(G_) k_rows_ws<G_.cw, G_.lw, G_.ppw, G_.ucap, G_.ncap, FMA, SADDR>
+template <bool FMA, bool SADDR> constexpr auto WS1 = SMFV_WS_INST(WS_GEOM1);
+template <bool FMA, bool SADDR> constexpr auto WS2 = SMFV_WS_INST(WS_GEOM2);
+template <bool FMA, bool SADDR> constexpr auto WS3 = SMFV_WS_INST(WS_GEOM3);
+#undef SMFV_WS_INST
 static auto pick_ws(int geom, bool fma, bool saddr)
 {
     if (geom == 2)
         return fma ? (saddr ? WS2<true, true> : WS2<true, false>) : (saddr ? WS2<false, true> : WS2<false, false>);
+    if (geom == 3)
+        return fma ? (saddr ? WS3<true, true> : WS3<true, false>) : (saddr ? WS3<false, true> : WS3<false, false>);
     return fma ? (saddr ? WS1<true, true> : WS1<true, false>) : (saddr ? WS1<false, true> : WS1<false, false>);
 }
 
-// ---------------------------------------------------------------------------
-// k_rows_cs: column-streamed tiles (K % 32 == 0; plan build_cs_plan).
-// One persistent 1024-lane block per CU (grid 8 x CS_BLOCKS_PER_XCD), two
-// tiles of ~m / 512 rows per block.  Compute waves 0-7 hold 32 rows each, two
-// lanes per row, 16 panel columns per lane in registers (8 x d2) for the
-// whole tile; the tile's X rows, sorted by column, stream through LDS in
-// chunks of <= CS_XCAP rows, double-buffered: loader waves 8-15 stage chunk
-// u + 1 (its X rows, then its values and u8 offsets) by LDS-DMA while the
-// compute waves run chunk u.  Per step every row of a wave takes one entry:
-// a 16-byte value read per two steps, a 4-byte offset read per four, and 8
-// b128 X reads; a lane reads its 8 X pieces rotated by its row slot (piece
-// (k + p) & 7 into accumulator k), so the 16 lanes of a b128 lane group hit
-// 16 different bank quads whatever X rows they read: no bank conflicts.
-// A row's entries of chunk c are a contiguous run of its column-sorted CSR
-// row, and chunks ascend by column, so each row is summed in CSR order
-// (separate multiply and add; pads: -0.0 on the zero image row): bit-
-// identical to the reference loop.  A row's Y is stored right after the
-// chunk holding its last entry (the plan's tlast), spreading the stores over
-// the tile.  One barrier per chunk.
-// ---------------------------------------------------------------------------
-namespace cs {
-constexpr int XSLOT = (CS_XCAP + 1) * 256;  // X image: chunk rows + the zero row
-constexpr int SL_M = 2 * XSLOT;             // meta slots (values, then aux) follow the X slots
-constexpr int MSLOT = CS_MV + CS_MA;
-constexpr int ZOFF = CS_XCAP * 256;
-static_assert(SL_M + 2 * MSLOT <= 160 * 1024, "two X and two meta slots must fit the CU's 160 KiB");
-static_assert(XSLOT % 1024 == 0 && MSLOT % 1024 == 0 && CS_MV % 1024 == 0, "1 KiB DMA pieces");
-static_assert((CS_XCAP + 3) / 4 <= 64, "8 X pieces per loader wave cover a chunk");
-}  // namespace cs
-
-struct CsXcd {
-    int first[9];  // XCD x runs tiles [first[x], first[x + 1]); block j of it runs tiles first + j, + 32, ...
-};
-template <bool FMA = false>
-__global__ __launch_bounds__(1024, 1) void k_rows_cs(CsXcd xr, int npanel, const int2 *__restrict__ bs,
-                                                     const int *__restrict__ trow, const int *__restrict__ tlast,
-                                                     const int *__restrict__ crec, const uint8_t *__restrict__ aux,
-                                                     const double *__restrict__ tv, const double *__restrict__ X,
-                                                     int64_t ldx, double *__restrict__ Y, int64_t ldy)
-{
-    using namespace ws;
-    using cs::XSLOT;
-    using cs::SL_M;
-    using cs::MSLOT;
-    __shared__ __attribute__((aligned(16))) char lds[SL_M + 2 * MSLOT];
-    const int nb = gridDim.x >> 3, x = blockIdx.x & 7;
-    const int t0 = xr.first[x] + (blockIdx.x >> 3), tend = xr.first[x + 1];
-    const int2 b = bs[blockIdx.x];  // the block's first chunk, its chunks per panel
-    const int nunits = b.y * npanel;
-    if (t0 >= tend || nunits == 0) return;  // block-uniform
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const unsigned lds0 = (unsigned)(uintptr_t)lds;
-    if (wv >= 8) {
-        // ---------------- loader waves ----------------
-        __builtin_amdgcn_s_setprio(3);
-        const int wl = wv - 8;
-        if (wl == 0 && lane < 32)  // zero row of both X slots
-            reinterpret_cast<d2 *>(lds + (lane >> 4) * XSLOT + cs::ZOFF)[lane & 15] = d2{0.0, 0.0};
-        i4 u0, u1, f0, f1;  // the chunk record: X-row ids of this lane's pieces, fields
-        const unsigned ldxb = (unsigned)(ldx * 8);
-        auto fetch_record = [&](int cid) {
-            const int *G = crec + (int64_t)cid * CS_CWORDS;
-            const i4 *gu = reinterpret_cast<const i4 *>(G + 32 * wl + 8 * (lane >> 4));
-            u0 = gu[0];
-            u1 = gu[1];
-            const i4 *gf = reinterpret_cast<const i4 *>(G + 256 + 8 * (lane & 15));
-            f0 = gf[0];  // nx, vb, nvp, ab
-            f1 = gf[1];  // nap, c, nch, next
-        };
-        // stage the record's chunk, panel p, into slot s
-        auto stage = [&](int p, int s) {
-            asm volatile("" ::"v"(u0), "v"(u1), "v"(f0), "v"(f1));
-            const int nx = f0.x, nvp = f0.z, nap = f1.x;
-            const unsigned xb = lds0 + s * XSLOT;
-            const int uc[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int piece = wl + 8 * i;  // 1 KiB = chunk rows 4 piece .. + 3
-                const int u = 4 * piece + (lane >> 4);
-                if (4 * piece < nx && u < nx)
-                    dma16s<false>(X + p * TILE_KP, (unsigned)uc[i] * ldxb + 16u * (unsigned)(lane & 15),
-                                  xb + piece * 1024);
-            }
-            const unsigned mb = lds0 + SL_M + s * MSLOT;
-            const double *tvb = tv + __builtin_amdgcn_readfirstlane(f0.y);
-            const uint8_t *ab = aux + __builtin_amdgcn_readfirstlane(f0.w);
-            for (int k = wl; k < nvp; k += 8) dma16s<true>(tvb, 1024u * k + 16u * lane, mb + k * 1024);
-            for (int k = wl; k < nap; k += 8) dma16s<true>(ab, 1024u * k + 16u * lane, mb + CS_MV + k * 1024);
-        };
-        // unit after the record's one: the next chunk of the tile, the
-        // tile's next panel, or the block's next tile
-        auto advance = [&](int &cid, int &p) {
-            const int c = f1.y, nch = f1.z, next = f1.w;
-            if (c + 1 < nch) {
-                ++cid;
-            } else if (p + 1 < npanel) {
-                cid -= c;
-                ++p;
-            } else {
-                cid = next;
-                p = 0;
-            }
-        };
-        int cid = b.x, p = 0;
-        fetch_record(cid);
-        stage(0, 0);
-        advance(cid, p);
-        if (nunits > 1) fetch_record(cid);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        barrier_lds();
-        for (int u = 0; u < nunits; ++u) {
-            if (u + 1 < nunits) {
-                stage(p, (u + 1) & 1);
-                advance(cid, p);
-                if (u + 2 < nunits) fetch_record(cid);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // unit u + 1 has landed
-            barrier_lds();
-        }
-        return;
-    }
-    // ---------------- compute waves ----------------
-    auto madd = [](d2 a, double v, d2 x) -> d2 {
-        if constexpr (FMA)
-            return d2{__builtin_fma(v, x.x, a.x), __builtin_fma(v, x.y, a.y)};
-        else
-            return a + v * x;
-    };
-    const int rp_ = lane >> 1, h = lane & 1, slot = wv * CS_RPW + rp_;
-    // accumulator k <-> this lane's X piece (k + p) & 7 of its half row: byte
-    // offset h * 128 + ((rot + 16 k) & 112) (two VALU per read, no registers)
-    const unsigned rot = (unsigned)((rp_ & 7) * 16), hoff = (unsigned)(h * 128);
-    int t = t0;
-    int rowc = trow[(int64_t)t * CS_ROWS + slot], lastc = tlast[(int64_t)t * CS_ROWS + slot];
-    int rown = -1, lastn = 0;
-    if (t + nb < tend) {
-        rown = trow[(int64_t)(t + nb) * CS_ROWS + slot];
-        lastn = tlast[(int64_t)(t + nb) * CS_ROWS + slot];
-    }
-    d2 acc[8];
-    barrier_lds();
-    int p = 0;
-    for (int u = 0; u < nunits; ++u) {
-        const char *xbase = lds + (u & 1) * XSLOT;
-        const char *mbase = lds + SL_M + (u & 1) * MSLOT;
-        const int *H = reinterpret_cast<const int *>(mbase + CS_MV);
-        const int S = __builtin_amdgcn_readfirstlane(H[4 * wv]);
-        const int vo = __builtin_amdgcn_readfirstlane(H[4 * wv + 1]);
-        const int lo = __builtin_amdgcn_readfirstlane(H[4 * wv + 2]);
-        const int c = __builtin_amdgcn_readfirstlane(H[CS_H_C]);
-        const int nch = __builtin_amdgcn_readfirstlane(H[CS_H_NCH]);
-        if (c == 0) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) acc[k] = d2{0.0, 0.0};
-        }
-        const d2 *V = reinterpret_cast<const d2 *>(mbase) + vo / 2 + rp_;  // [s / 2][row] pairs
-        // software pipeline by half steps (4 of a step's 8 X pieces): the
-        // reads of the next half go out before the FP64 of this one (two
-        // ping-pong sets of 4 x d2); the values and offsets of a step pair
-        // are read a pair ahead (S is even).  Reads past the wave's last step
-        // (stale offsets) stay inside the block's LDS and are never summed.
-        const unsigned short *L = reinterpret_cast<const unsigned short *>(mbase + CS_MV + lo) + rp_;  // [s / 2][row]
-        auto load_h = [&](d2 *xv, unsigned o, int half) {
-            const char *xr_ = xbase + o * 256 + hoff;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                xv[k] = *reinterpret_cast<const d2 *>(xr_ + ((rot + 16u * (4 * half + k)) & 112u));
-        };
-        // one term = multiply then add (the reference's rounding), kept as
-        // one asm unit so the scheduler cannot hoist the multiplies ahead of
-        // their adds (more live registers)
-        auto fma4 = [&](double v, const d2 *xv, int half) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                d2 &a = acc[4 * half + k];
-                if constexpr (FMA) {
-                    a = madd(a, v, xv[k]);
-                } else {
-                    double t0, t1;
-                    asm("v_mul_f64 %0, %4, %5\n\tv_mul_f64 %1, %4, %6\n\t"
-                        "v_add_f64 %2, %2, %0\n\tv_add_f64 %3, %3, %1"
-                        : "=&v"(t0), "=&v"(t1), "+v"(a.x), "+v"(a.y)
-                        : "v"(v), "v"(xv[k].x), "v"(xv[k].y));
-                }
-            }
-        };
-        if (S > 0) {
-            d2 xa[4], xb[4];
-            d2 vP = V[0];
-            unsigned oP = L[0];
-            load_h(xa, oP & 0xFF, 0);
-            for (int i = 1;; ++i) {
-                load_h(xb, oP & 0xFF, 1);
-                __builtin_amdgcn_sched_barrier(0);
-                fma4(vP.x, xa, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                load_h(xa, oP >> 8, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                fma4(vP.x, xb, 1);
-                __builtin_amdgcn_sched_barrier(0);
-                const d2 vN = V[32 * i];
-                const unsigned oN = L[32 * i];
-                load_h(xb, oP >> 8, 1);
-                __builtin_amdgcn_sched_barrier(0);
-                fma4(vP.y, xa, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                if (2 * i >= S) {
-                    fma4(vP.y, xb, 1);
-                    break;
-                }
-                load_h(xa, oN & 0xFF, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                fma4(vP.y, xb, 1);
-                __builtin_amdgcn_sched_barrier(0);
-                vP = vN;
-                oP = oN;
-            }
-        }
-        if (rowc >= 0 && lastc == c) {
-            double *y = Y + (int64_t)rowc * ldy + p * TILE_KP + h * 16;
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                __builtin_nontemporal_store(acc[k], reinterpret_cast<d2 *>(y + ((rot + 16u * k) & 112u) / 8));
-        }
-        if (c == nch - 1 && ++p == npanel) {
-            p = 0;
-            t += nb;
-            rowc = rown;
-            lastc = lastn;
-            if (t + nb < tend) {
-                rown = trow[(int64_t)(t + nb) * CS_ROWS + slot];
-                lastn = tlast[(int64_t)(t + nb) * CS_ROWS + slot];
-            }
-        }
-        barrier_lds();  // slot (u & 1) is free for unit u + 2
-    }
-}
+#ifdef SMFV_LAB
+#include "lab/cs_lab.inc"  // k_rows_cs, column-streamed tiles (lab only since r4: measured 3.4x slower)
+#endif
 
 // Rows the ws plan could not tile (over a cap alone): one 8-lane team per
 // row, X gathered straight from HBM, CSR order (bit-identical).  `rows` are
@@ -1868,8 +1645,11 @@ static TileCaps plan_caps(int flags, int col_base)
 {
     TileCaps caps;
     // (r4) the k_rows_ws geometry the tiles are cut for (WsGeom)
-    const int g = (flags & SMFV_PLAN_WS_GEOM2) ? 2 : (flags & SMFV_PLAN_WS_GEOM1) ? 1 : SMFV_WS_DEFAULT_GEOM;
-    caps.geom = g == 2 ? WS_GEOM2 : WS_GEOM1;
+    const int g = (flags & SMFV_PLAN_WS_GEOM3)   ? 3
+                  : (flags & SMFV_PLAN_WS_GEOM2) ? 2
+                  : (flags & SMFV_PLAN_WS_GEOM1) ? 1
+                                                 : SMFV_WS_DEFAULT_GEOM;
+    caps.geom = ws_geom(g);
     caps.ucap = caps.geom.ucap;
     caps.ncap = caps.geom.ncap - 3 * caps.geom.rows();  // room for the quads' interleave padding
     caps.maxrows = caps.geom.rows();
@@ -1922,7 +1702,7 @@ struct smfv_plan_s {
     int64_t snapshot = 0;                  // values gathered by bind (tile entries + slack + direct rows)
     double reuse = 0.0, est_reuse = -1.0, analysis_ms = 0.0;
     int ws_xcd[9] = {};            // XCD x runs tiles [ws_xcd[x], ws_xcd[x + 1])
-    int ws_geom = 0;               // (r4) k_rows_ws geometry: 1 (WS_GEOM1) or 2 (WS_GEOM2)
+    int ws_geom = 0;               // (r4) k_rows_ws geometry: WsGeom::id (1, 2, 3)
     int parts = 1;                 // 8: one part of the rows per XCD (build_ws_plan)
     double footprint = -1.0;       // parts_footprint of the 8 parts
     int *tsrc = nullptr;                   // snapshot entry -> CSR index of its value (-1: pad)
@@ -2073,6 +1853,8 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                 }
             }
         }
+#ifdef SMFV_LAB
+        // (lab only since r4)
         // column-streamed tiles (k_rows_cs) where asked for; a pattern the
         // layout does not take (unsorted rows, ...) keeps k_rows_ws
         if (!rc && go && !(flags & SMFV_PLAN_MFMA) && (flags & SMFV_PLAN_CS) && !(flags & SMFV_PLAN_WS)) {
@@ -2113,13 +1895,14 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                 }
             }
         }
+#endif
         if (!rc && go && !p->mfma && !p->cs && !(flags & SMFV_PLAN_MFMA)) {
             WsPlan W;
             std::string err;
             // a pattern the tile layout cannot take (the replayed plan fails its
             // checks) keeps the untiled plan rather than failing the create
             if (build_ws_plan(m, n, rpl.data(), cil, W, &err, caps)) {
-                p->ws_geom = W.geom.cw == 4 ? 2 : 1;
+                p->ws_geom = W.geom.id;
                 p->ntiles = W.ntiles;
                 for (int x = 0; x <= 8; ++x) p->ws_xcd[x] = W.xcd[x];
                 p->parts = caps.part_start.size() > 2 ? (int)caps.part_start.size() - 1 : 1;
@@ -2302,7 +2085,7 @@ SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int
         for (int t = W.xcd[x]; t < W.xcd[x + 1]; ++t) {
             const int *G = &W.grec[(size_t)t * WS_GWORDS];
             for (int u = 0; u < G[WS_G_NU]; ++u) {
-                const int c = G[32 * ((u / 4) % 8) + 8 * (u % 4) + (u / 4) / 8];
+                const int c = G[W.geom.gword((u / 4) % W.geom.lw, u % 4, (u / 4) / W.geom.lw)];
                 if (stamp[c] != x) stamp[c] = x, ++sum;
             }
         }
@@ -2313,6 +2096,7 @@ SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int
     return SMFV_OK;
 }
 
+#ifdef SMFV_LAB  // lab only since r4 (csrc/lab/cs_plan_lab.h)
 SMFV_API int smfv_cs_plan_analyse(int row_begin, int row_end, int n, const int *h_row_ptr_all,
                                   const int *h_col_idx_all, int flags, int rows_per_tile, double out[8])
 {
@@ -2355,6 +2139,7 @@ SMFV_API int smfv_cs_plan_analyse(int row_begin, int row_end, int n, const int *
     out[7] = steps;
     return SMFV_OK;
 }
+#endif
 
 SMFV_API int smfv_spmv_chunks_analyse(int row_begin, int row_end, int n, const int *h_row_ptr_all,
                                       const int *h_col_idx_all, int cap, double out[6])
@@ -2500,6 +2285,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         int v = 0;
         if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
     }
+#ifdef SMFV_LAB  // k_rows_cs: lab only since r4
     if (plan->cs) {
         // 8 x 32 persistent blocks (the plan's per-block chunk lists assume
         // that grid; on a chip with fewer CUs blocks queue, still correct);
@@ -2516,6 +2302,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         SMFV_LAUNCHED();
         return SMFV_OK;
     }
+#endif
     if (plan->mfma) {
         if (plan->ntiles > 0) {
             hipLaunchKernelGGL(k_rows_mfma, dim3((unsigned)plan->ntiles), dim3(256), 0, st, K / TILE_KP, plan->mf_rec,
@@ -2525,7 +2312,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     } else if (plan->ntiles > 0) {
         // persistent blocks: one (geometry 1) or two (geometry 2) per CU; a
         // multiple of 8 (>= 8) so every XCD's tile range has blocks
-        const int per_cu = plan->ws_geom == 2 ? 2 : 1;
+        const int per_cu = ws_geom(plan->ws_geom).cw == 4 ? 2 : 1;
         const int blocks = std::max(8, (std::min(plan->ntiles, per_cu * ncu) + 7) & ~7);
         int chunked = SMFV_WS_CHUNKED;
         // scalar-base addressing when X (n rows of ldx doubles) and the
@@ -2556,7 +2343,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
                   : abl == 11 ? (K == TILE_KP ? k_rows_ws_lab<11> : WS1<false, true>)
                   : abl == 17 ? (K == TILE_KP && plan->m >= 120000 ? k_rows_ws_lab<17> : WS1<false, true>) : WS1<false, true>;
         // the lab's ablation copies are geometry 1 only
-        if (!(saddr && lab_saddr) || plan->ws_geom == 2) kern = pick_ws(plan->ws_geom, plan->fma, saddr && lab_saddr);
+        if (!(saddr && lab_saddr) || plan->ws_geom != 1) kern = pick_ws(plan->ws_geom, plan->fma, saddr && lab_saddr);
         static unsigned long long *stamp_buf = nullptr;
         const size_t stamp_n = (size_t)blocks * 16 * WS_STAMP_UNITS * 2;
         if (abl == 8 && !stamp_buf) {
@@ -2570,7 +2357,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
 #endif
         WsXcd xr;
         for (int x = 0; x <= 8; ++x) xr.first[x] = plan->ws_xcd[x];
-        const int threads = plan->ws_geom == 2 ? WS_GEOM2.threads() : WS_GEOM1.threads();
+        const int threads = ws_geom(plan->ws_geom).threads();
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3((unsigned)threads), 0, st, xr, K / TILE_KP, chunked,
                            plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();

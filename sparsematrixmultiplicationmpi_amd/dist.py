@@ -128,16 +128,25 @@ class DistPlan:
     comm=None with rank=(r, p): the plan of rank r of p alone, no
     communicator (smfv_dist_plan_create_rank): run_local() computes what that
     rank of the reference's variant computes, into Y (ROWWISE) or the plan's
-    exchange buffer (exchange_buffer()); exchange() is refused."""
+    exchange buffer (exchange_buffer()); exchange() is refused.
+
+    Values: a tiled share (and every K = 1 chunk plan) computes with the
+    snapshot of A's values taken by the last bind; run() / run_local() bind
+    again by themselves when A's values tensor changed in place since (its
+    version counter), as SpmmPlan does through DeviceCSR.plan()."""
 
     def __init__(self, comm: Communicator | None, variant: int, A: DeviceCSR, K: int, to_all: bool,
                  root: int = 0, tiles: str = "auto", rowpart: bool = False, m: int | None = None,
-                 stream=None, rank: tuple[int, int] | None = None, fma: bool = False):
+                 stream=None, rank: tuple[int, int] | None = None, fma: bool = False, tiled_kernel: str = "auto"):
         self.comm, self.variant, self.A, self.K = comm, Variant(variant), A, K
         self.mode = TO_ALL if to_all else TO_ROOT
         self.root = root
         self.m = A.m if not rowpart else int(m)
+        from .engine import PLAN_WS, PLAN_WS_GEOM1, PLAN_WS_GEOM2, PLAN_WS_GEOM3
         flags = {"auto": 0, "off": 1, "force": 2}[tiles] | (4 if fma else 0)
+        # the rank share's tiled-kernel geometry (SpmmPlan's tiled_kernel; A/B)
+        flags |= {"auto": 0, "ws1": PLAN_WS | PLAN_WS_GEOM1, "ws2": PLAN_WS | PLAN_WS_GEOM2,
+                  "ws3": PLAN_WS | PLAN_WS_GEOM3}[tiled_kernel]
         ip = POINTER(c_int)
         self._h = c_void_p()
         if comm is None:
@@ -154,6 +163,11 @@ class DistPlan:
 
     def bind_values(self, stream=None) -> None:
         call("smfv_dist_plan_bind_values", self._h, self.A.values.data_ptr(), stream_handle(stream))
+        self.bound_version = self.A.values_version()
+
+    def _rebind_if_changed(self, stream) -> None:
+        if self.A.values_version() != self.bound_version:
+            self.bind_values(stream)
 
     def _check(self, X: torch.Tensor, Y: torch.Tensor) -> None:
         if X.shape != (self.A.n, self.K) or not X.is_contiguous() or X.dtype != torch.float64:
@@ -163,6 +177,7 @@ class DistPlan:
 
     def run(self, X: torch.Tensor, Y: torch.Tensor, stream=None) -> torch.Tensor:
         self._check(X, Y)
+        self._rebind_if_changed(stream)
         rp, ci, va = self.A.ptrs()
         call("smfv_dist_plan_execute", self._h, rp, ci, va, X.data_ptr(), Y.data_ptr(), stream_handle(stream))
         return Y
@@ -170,6 +185,7 @@ class DistPlan:
     def run_local(self, X: torch.Tensor, Y: torch.Tensor, stream=None) -> torch.Tensor:
         """The rank-local compute alone (no exchange)."""
         self._check(X, Y)
+        self._rebind_if_changed(stream)
         rp, ci, va = self.A.ptrs()
         call("smfv_dist_plan_execute_local", self._h, rp, ci, va, X.data_ptr(), Y.data_ptr(),
              stream_handle(stream))
@@ -198,7 +214,7 @@ class DistPlan:
         call("smfv_dist_plan_stats", self._h, out)
         return {"tiled": bool(out[0]), "tiles": int(out[1]), "reuse": float(out[3]),
                 "row_begin": int(out[6]), "analysis_ms": float(out[8]), "xcd_parts": int(out[11]),
-                "footprint": float(out[12])}
+                "footprint": float(out[12]), "ws_geom": int(out[15])}
 
     def __del__(self):
         try:

@@ -117,7 +117,7 @@ def _check_dense(T: torch.Tensor, rows: int, K: int, name: str) -> int:
 
 PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA, PLAN_NATURAL_SEEDS, PLAN_MFMA, PLAN_SPLIT_ENDS = 1, 2, 4, 8, 16, 32
 PLAN_ONE_WAVEFRONT, PLAN_SIMPLE_ROWS, PLAN_CS, PLAN_WS = 64, 128, 256, 512
-PLAN_WS_GEOM1, PLAN_WS_GEOM2 = 1024, 2048
+PLAN_WS_GEOM1, PLAN_WS_GEOM2, PLAN_WS_GEOM3 = 1024, 2048, 4096
 PLAN_STATS = 16  # SMFV_PLAN_STATS
 PLAN_KERNELS = {0: None, 1: "k_rows_ws", 2: "k_rows_mfma", 3: "k_spmv_chunks", 4: "k_rows_cs"}
 
@@ -158,7 +158,7 @@ class SpmmPlan:
         # A/B; "ws1" / "ws2": k_rows_ws with one 1024-lane / two 512-lane
         # pipelines per CU (SMFV_PLAN_WS_GEOM1 / GEOM2)
         flags |= {"auto": 0, "cs": PLAN_CS, "ws": PLAN_WS, "ws1": PLAN_WS | PLAN_WS_GEOM1,
-                  "ws2": PLAN_WS | PLAN_WS_GEOM2}[tiled_kernel]
+                  "ws2": PLAN_WS | PLAN_WS_GEOM2, "ws3": PLAN_WS | PLAN_WS_GEOM3}[tiled_kernel]
         self._plan = ctypes.c_void_p()
         ip = ctypes.POINTER(ctypes.c_int)
         if rows is None:

@@ -744,6 +744,22 @@ def test_mfma_tile_kernel_within_tolerance(gpu, K):
         assert np.all(np.abs(Y.cpu().numpy() - Yref) <= 1e-12 * scale + 1e-300)
 
 
+def test_column_streamed_flag_ignored_by_the_product(gpu):
+    """(r4) k_rows_cs is lab-only: in libsmfv.so SMFV_PLAN_CS is ignored and
+    the plan runs k_rows_ws, bit-identical to the reference order."""
+    if smfv._lib.LAB:
+        pytest.skip("the lab build keeps k_rows_cs")
+    A = smfv.gen_fem27(6000, 20, 20, 0.83, 3)
+    X = np.random.default_rng(3).uniform(-1, 1, (A.numCols, 32))
+    plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(A, gpu), 32, tiles="force", tiled_kernel="cs")
+    assert plan.stats()["kernel"] == "k_rows_ws"
+    Y = torch.full((A.numRows, 32), np.nan, dtype=torch.float64, device=gpu)
+    plan.run(torch.from_numpy(X).to(gpu), Y)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(Y.cpu().numpy()), bits(oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)))
+
+
+@pytest.mark.skipif(not smfv._lib.LAB, reason="lab build only (SMFV_LAB=1 loads libsmfv_lab.so)")
 @pytest.mark.parametrize("K", [32, 64])
 def test_column_streamed_tiles_opt_in(gpu, K):
     """Opt-in SMFV_PLAN_CS (k_rows_cs, measured slower than k_rows_ws and not

@@ -241,6 +241,46 @@ def test_ws_plan_tiny_and_empty_rows():
         assert out[5] == nnz and out[4] % 8 == 0 and nnz <= out[4] <= 32 * A.numRows, (name, list(out))
 
 
+def test_ws_geometry2_plans_verify():
+    """(r4) Geometry 2 of k_rows_ws (two 512-lane pipelines per CU,
+    SMFV_PLAN_WS_GEOM2): tiles of <= 32 rows and <= 125 staged X rows, built
+    and verified natively (the replay of the kernel's reads, with its 32-slot
+    record and 4 loader waves) on the stand-ins and on tiny, empty-row and
+    unsorted patterns.  Geometry 1 stays what it was."""
+    G1, G2 = 1024, 2048  # SMFV_PLAN_WS_GEOM1 / GEOM2
+    A = smfv.cop20k_surrogate()
+    g1, g2 = _analyse_rows(A, 0, A.numRows, G1), _analyse_rows(A, 0, A.numRows, G2)
+    assert g1 == _analyse_rows(A, 0, A.numRows)  # the default is geometry 1
+    assert g1["tiles"] == 2011 and g2["direct"] == 0
+    assert 2.4 * g1["tiles"] < g2["tiles"] < 2.7 * g1["tiles"] and g2["reuse"] > 4.0
+    for name in ("empty7x5.mtx", "pat4x6.mtx"):
+        B = smfv.readMatrixMarketFile(os.path.join(GOLDEN, name))
+        assert _analyse_rows(B, 0, B.numRows, G2)["tiles"] >= 1, name
+    # a row block starting mid-matrix (a rank's share)
+    assert _analyse_rows(A, 50_000, 70_000, G2)["tiles"] >= 20_000 / 32
+
+
+def test_tile_analysis_unsorted_rows_with_repeats():
+    """a row whose repeated column is not adjacent (unsorted CSR
+    rows) must not undercount the tile's union; the plan still verifies
+    (every row's entries in CSR order) in both geometries."""
+    rng = np.random.default_rng(5)
+    m = 3000
+    rows = []
+    for r in range(m):
+        cols = [(r + d) % m for d in (-2, -1, 0, 1, 2)] + [(r + 1) % m, (r - 2) % m]  # repeats, unsorted
+        rng.shuffle(cols)
+        rows.append(cols)
+    rp = np.zeros(m + 1, dtype=np.int32)
+    rp[1:] = np.cumsum([len(c) for c in rows])
+    ci = np.concatenate(rows).astype(np.int32)
+    out = (ctypes.c_double * 9)()
+    ip = ctypes.POINTER(ctypes.c_int)
+    for flags in (1024, 2048):
+        _lib.call("smfv_plan_analyse_rows", 0, m, m, rp.ctypes.data_as(ip), ci.ctypes.data_as(ip), flags, out)
+        assert out[0] >= 1 and out[5] == len(ci), (flags, list(out))
+
+
 def test_xcd_parts_cut_compulsory_x_traffic():
     """Each XCD has its own L2: the plan splits the rows into 8 parts (row
     ranges or breadth-first shares, whichever reads fewer X rows) and runs
@@ -499,6 +539,19 @@ def test_spmv_chunk_layout():
     assert np.diff(P.rowPtr).max() > 2048 and not _chunks(P, cap=2048)["fits"]
 
 
+def test_column_streamed_plan_is_lab_only():
+    """(r4) The column-streamed tile kernel (k_rows_cs, measured 3.4x slower)
+    lives in the lab build only: libsmfv.so exports no k_rows_cs symbol and no
+    smfv_cs_plan_analyse; libsmfv_lab.so keeps both for A/B."""
+    nm = subprocess.run(["nm", "-D", "-C", os.path.join(PKG, "libsmfv.so")], capture_output=True, text=True).stdout
+    assert "smfv_cs_plan_analyse" not in nm and "k_rows_cs" not in nm
+    lab = os.path.join(PKG, "libsmfv_lab.so")
+    if os.path.exists(lab):
+        nm = subprocess.run(["nm", "-D", lab], capture_output=True, text=True).stdout
+        assert "smfv_cs_plan_analyse" in nm
+
+
+@pytest.mark.skipif(not _lib.LAB, reason="lab build only (SMFV_LAB=1 loads libsmfv_lab.so)")
 def test_column_streamed_plan_layout():
     """The opt-in column-streamed tile plan (k_rows_cs, SMFV_PLAN_CS), built and
     verified natively (every row's entries replayed chunk by chunk in CSR
