@@ -898,6 +898,8 @@ def main() -> None:
                          "(for a cold-only rocprofv3 kernel trace)")
     ap.add_argument("--no-copy-floor", action="store_true",
                     help="skip the size-matched copy (roofline.size_matched_copy)")
+    ap.add_argument("--no-rebind", action="store_true",
+                    help="skip the bind + execute leg (values changed every step; plan.rebind_each_step)")
     ap.add_argument("--no-check", action="store_true",
                     help="report the post-timing result check but do not fail on it (lab ablations)")
     ap.add_argument("--mfma", action="store_true",
@@ -1020,12 +1022,45 @@ def main() -> None:
 
     stabilize_replays = []
 
+    st0 = copies[0][0].stats()
     g_cold = capture(False)
     span_ms = timed(g_cold)
     # nine more samples of the same K steps (median of 10), reported
     # beside `value`, which stays the first timed region
     samples = sorted([span_ms] + [timed(g_cold) for _ in range(9)])
     del g_cold
+    # bind + execute per step with the values changed every step (an
+    # iterative caller whose matrix values change between products): each
+    # copy alternates between two value arrays, every step re-binds its plan
+    # (the values snapshot) and runs it, all in one graph; the bind alone
+    # the same way.  Reported in `plan`, not in `value`.
+    rebind = None
+    if not args.no_rebind:
+        from sparsematrixmultiplicationmpi_amd._lib import call as _call
+        alt = [(plan.A.values, plan.A.values * 0.5 + 1.0) for plan, _, _ in copies]
+        torch.cuda.synchronize()
+
+        def rb_step(i, execute=True):
+            plan, dX, dY = copies[i % ncopies]
+            vals = alt[i % ncopies][(i // ncopies) % 2]
+            st_ = torch.cuda.current_stream().cuda_stream
+            _call("smfv_plan_bind_values", plan._plan, vals.data_ptr(), st_)
+            if execute:
+                rp_, ci_, _ = plan.A.ptrs()
+                _call("smfv_plan_execute", plan._plan, rp_, ci_, vals.data_ptr(), dX.data_ptr(), K, dY.data_ptr(), K,
+                      st_)
+        ms_be, how_be = _graph_or_eager(lambda i: rb_step(i, True), args.steps, world)
+        ms_b, _ = _graph_or_eager(lambda i: rb_step(i, False), args.steps, world)
+        for plan, _, _ in copies:  # back to the values the check uses
+            plan.bind_values()
+        torch.cuda.synchronize()
+        rebind = {"bind_plus_execute_ms": round(ms_be, 6), "bind_ms": round(ms_b, 6),
+                  "bind_descriptors": st0.get("bind_descriptors"),
+                  "GFLOPs_incl_bind": round(2.0 * nnz * K / (ms_be * 1e-3) / 1e9, 3),
+                  "frac_incl_bind": round(prob_bytes / (ms_be * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                  "timing": how_be,
+                  "note": "every step binds its plan to values that changed since its last bind (two arrays "
+                          "alternating per copy) and executes; bind_ms: the binds alone, same rotation"}
     # the warm leg (same copy every launch) after the cold one; --no-warm
     # leaves it out so a profile of this process holds cold launches only
     span_ms_w = timed(capture(True)) if not args.no_warm else float("nan")
@@ -1106,6 +1141,7 @@ def main() -> None:
                      "est_reuse_sampled": round(st["est_reuse"], 3), "direct_rows": st["direct_rows"],
                      "create_s": round(t_plan[0], 3), "analysis_ms": round(st["analysis_ms"], 1),
                      "bind_ms": round(bind_ms, 4), "snapshot_entries": st["snapshot_entries"],
+                     "rebind_each_step": rebind,
                      "xcd_parts": st["xcd_parts"], "footprint_8_ranges": round(st["footprint"], 3),
                      "note": "create = host analysis + upload, once per pattern; bind = values snapshot "
                              "gather, once per value change; neither is in the timed step"},

@@ -993,6 +993,43 @@ __global__ __launch_bounds__(256) void k_gather_vals(int64_t count, const int *_
     }
 }
 
+// (r4) The bind from descriptors: only the real entries of the snapshot are
+// written (its pads were filled once at plan creation, k_fill_f64), and the
+// sources come from per-quad / per-run descriptors instead of a per-entry
+// int32 index: 16 B moved per non-zero instead of 28 per snapshot entry.
+// Quad q (WS_QWORDS... expanded to 10 ints on the host: first pair, pairs,
+// then (CSR start, length) of its 4 rows): pair j holds entries 2 (j / 4),
+// +1 of row j % 4.  One wave per quad.
+__global__ __launch_bounds__(256) void k_bind_quads(int64_t nq, const int *__restrict__ qd,
+                                                    const double *__restrict__ va, double *__restrict__ tv)
+{
+    const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (qi >= nq) return;
+    const int *d = qd + qi * 10;
+    const int pb = d[0], np = d[1];
+    for (int j = threadIdx.x & 63; j < np; j += 64) {
+        const int k = j & 3, el = (j >> 2) * 2;
+        const int src = d[2 + 2 * k], len = d[3 + 2 * k];
+        double *o = tv + 2 * ((int64_t)pb + j);
+        if (el + 1 < len)
+            *reinterpret_cast<ws::d2 *>(o) = ws::d2{va[src + el], va[src + el + 1]};
+        else if (el < len)
+            o[0] = va[src + el];
+    }
+}
+// contiguous runs (direct rows, K = 1 chunks): {dst entry, src, count}, one block per run
+__global__ __launch_bounds__(256) void k_bind_runs(const int64_t *__restrict__ rd, const double *__restrict__ va,
+                                                   double *__restrict__ tv)
+{
+    const int64_t *d = rd + 3 * (int64_t)blockIdx.x;
+    const int64_t dst = d[0], src = d[1], cnt = d[2];
+    for (int64_t i = threadIdx.x; i < cnt; i += 256) tv[dst + i] = va[src + i];
+}
+__global__ __launch_bounds__(256) void k_fill_f64(int64_t n, double v, double *__restrict__ out)
+{
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) out[i] = v;
+}
+
 // ---------------------------------------------------------------------------
 // k_merge: nnz-balanced merge-path over the rows [row_first, row_first +
 // nrows) restricted to nnz [s, e).  The merge list is {row ends} x {nnz};
@@ -1705,7 +1742,11 @@ struct smfv_plan_s {
     int ws_geom = 0;               // (r4) k_rows_ws geometry: WsGeom::id (1, 2, 3)
     int parts = 1;                 // 8: one part of the rows per XCD (build_ws_plan)
     double footprint = -1.0;       // parts_footprint of the 8 parts
-    int *tsrc = nullptr;                   // snapshot entry -> CSR index of its value (-1: pad)
+    int *tsrc = nullptr;                   // snapshot entry -> CSR index of its value (-1: pad); NULL with descriptors
+    int *bind_quads = nullptr;             // (r4) bind descriptors: 10 ints per quad (k_bind_quads)
+    int64_t *bind_runs = nullptr;          // (r4) 3 int64 per contiguous run (k_bind_runs)
+    int64_t nbind_quads = 0, nbind_runs = 0;
+    bool bind_desc = false;                // bind from the descriptors (pads filled at creation)
     double *tvals = nullptr;               // the bound values snapshot (tile order, pads -0.0, then direct rows)
     const double *bound_values = nullptr;  // d_values the snapshot came from
     int *ws_grec = nullptr, *ws_lrec = nullptr, *direct_rows = nullptr;
@@ -1731,7 +1772,7 @@ struct smfv_plan_s {
     hipStream_t bind_stream = nullptr;
     ~smfv_plan_s()
     {
-        for (void *q : {(void *)tsrc, (void *)tvals, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
+        for (void *q : {(void *)tsrc, (void *)bind_quads, (void *)bind_runs, (void *)tvals, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
                         (void *)direct_off, (void *)ws_loff, ws, (void *)mf_rec, (void *)mf_ucols, (void *)mf_bstep,
                         (void *)k1_hdr, (void *)k1_rs, (void *)k1_off, (void *)k1_col, (void *)cs_bs,
                         (void *)cs_trow, (void *)cs_tlast, (void *)cs_crec, (void *)cs_aux})
@@ -1751,6 +1792,64 @@ template <class T> int upload(T **dst, const std::vector<T> &src, size_t &acc)
 }
 
 }  // namespace
+
+// (r4) The snapshot's sources as bind descriptors (quads of the tiled layout,
+// contiguous runs), checked on the host against the per-entry sources `ts`
+// (each real entry once, from the same CSR index; pads untouched).  On a
+// match the descriptors are uploaded and the pads written once; otherwise
+// the plan keeps the per-entry gather (k_gather_vals over ts).
+static int setup_bind(smfv_plan_s *p, const std::vector<int> &ts, const std::vector<int> &quads,
+                      const std::vector<int64_t> &runs, double pad)
+{
+    const int64_t n = (int64_t)ts.size();
+    std::vector<int> chk((size_t)n, -1);
+    bool ok = true;
+    for (size_t q = 0; ok && q < quads.size() / 10; ++q) {
+        const int *d = &quads[q * 10];
+        for (int j = 0; ok && j < d[1]; ++j) {
+            const int k = j & 3, el = (j >> 2) * 2;
+            for (int h = 0; h < 2 && ok; ++h)
+                if (el + h < d[3 + 2 * k]) {
+                    const int64_t e = 2 * ((int64_t)d[0] + j) + h;
+                    ok = e < n && chk[(size_t)e] == -1;
+                    if (ok) chk[(size_t)e] = d[2 + 2 * k] + el + h;
+                }
+        }
+    }
+    for (size_t r = 0; ok && r < runs.size() / 3; ++r)
+        for (int64_t i = 0; ok && i < runs[3 * r + 2]; ++i) {
+            const int64_t e = runs[3 * r] + i;
+            ok = e < n && chk[(size_t)e] == -1;
+            if (ok) chk[(size_t)e] = (int)(runs[3 * r + 1] + i);
+        }
+    ok = ok && chk == ts;
+    int rc = SMFV_OK;
+    if (ok) {
+        p->bind_desc = true;
+        p->nbind_quads = (int64_t)quads.size() / 10;
+        p->nbind_runs = (int64_t)runs.size() / 3;
+        rc = upload(&p->bind_quads, quads, p->dev_bytes);
+        if (!rc) rc = upload(&p->bind_runs, runs, p->dev_bytes);
+    } else {
+        rc = upload(&p->tsrc, ts, p->dev_bytes);
+    }
+    if (!rc) {
+        const size_t b = std::max<size_t>((size_t)n, 1) * sizeof(double);
+        SMFV_HIP(hipMalloc(reinterpret_cast<void **>(&p->tvals), b));
+        p->dev_bytes += b;
+        if (ok && n > 0) {  // the pads, once, on a private stream (create is synchronous)
+            hipStream_t fs = nullptr;
+            SMFV_HIP(hipStreamCreateWithFlags(&fs, hipStreamNonBlocking));
+            hipLaunchKernelGGL(k_fill_f64, dim3((unsigned)std::min<int64_t>((n + 255) / 256, 4096)), dim3(256), 0, fs,
+                               n, pad, p->tvals);
+            hipError_t e = hipGetLastError();
+            if (e == hipSuccess) e = hipStreamSynchronize(fs);
+            (void)hipStreamDestroy(fs);
+            SMFV_HIP(e);
+        }
+    }
+    return rc;
+}
 
 // Plan of rows [row_begin, row_begin + m) of a CSR matrix: h_rp / h_ci are the
 // host arrays of the WHOLE matrix (or NULL: no tiling); the analysis runs on
@@ -1924,17 +2023,29 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                         for (int j = rpl[r]; j < rpl[r + 1]; ++j) ts.push_back((int)(nnz_base + j));
                     }
                     p->snapshot = (int64_t)ts.size();
+                    // bind descriptors: the quads (CSR start and length of their rows), the direct rows
+                    std::vector<int> qd;
+                    qd.reserve(W.quads.size() / WS_QWORDS * 10);
+                    for (size_t q = 0; q < W.quads.size(); q += WS_QWORDS) {
+                        qd.push_back(W.quads[q]);
+                        qd.push_back(W.quads[q + 1]);
+                        for (int k = 0; k < 4; ++k) {
+                            const int r = W.quads[q + 2 + k];
+                            qd.push_back(r >= 0 ? (int)(nnz_base + rpl[r]) : 0);
+                            qd.push_back(r >= 0 ? rpl[r + 1] - rpl[r] : 0);
+                        }
+                    }
+                    std::vector<int64_t> runs;
+                    for (size_t i = 0; i < W.direct.size(); ++i) {
+                        const int r = W.direct[i];
+                        runs.insert(runs.end(), {doff[i], nnz_base + rpl[r], (int64_t)(rpl[r + 1] - rpl[r])});
+                    }
                     if (!rc) rc = upload(&p->ws_grec, W.grec, p->dev_bytes);
                     if (!rc) rc = upload(&p->ws_lrec, W.lrec, p->dev_bytes);
                     if (!rc) rc = upload(&p->ws_loff, W.loff, p->dev_bytes);
-                    if (!rc) rc = upload(&p->tsrc, ts, p->dev_bytes);
                     if (!rc) rc = upload(&p->direct_rows, W.direct, p->dev_bytes);
                     if (!rc) rc = upload(&p->direct_off, doff, p->dev_bytes);
-                    if (!rc) {
-                        const size_t b = std::max<size_t>((size_t)p->snapshot, 1) * sizeof(double);
-                        fail_hip(hipMalloc(reinterpret_cast<void **>(&p->tvals), b), "hipMalloc(tvals)");
-                        p->dev_bytes += b;
-                    }
+                    if (!rc) rc = setup_bind(p, ts, qd, runs, -0.0);
                 }
             }
         }
@@ -1957,15 +2068,16 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
             for (int &q : C.tsrc)
                 if (q >= 0) q += (int)nnz_base;
             p->snapshot = (int64_t)C.tsrc.size();
+            // bind descriptors: each chunk's entries are one contiguous CSR run
+            std::vector<int64_t> runs;
+            for (int c = 0; c < C.nchunks; ++c) {
+                const int64_t cnt = C.hdr[(size_t)c * 4 + 3], dst = (int64_t)c * C.cap;
+                if (cnt > 0) runs.insert(runs.end(), {dst, (int64_t)C.tsrc[(size_t)dst], cnt});
+            }
             if (!rc) rc = upload(&p->k1_hdr, C.hdr, p->dev_bytes);
             if (!rc) rc = upload(&p->k1_rs, C.rs, p->dev_bytes);
             if (!rc) rc = C.wide ? upload(&p->k1_col, C.col, p->dev_bytes) : upload(&p->k1_off, C.off, p->dev_bytes);
-            if (!rc) rc = upload(&p->tsrc, C.tsrc, p->dev_bytes);
-            if (!rc) {
-                const size_t b = std::max<size_t>((size_t)p->snapshot, 1) * sizeof(double);
-                fail_hip(hipMalloc(reinterpret_cast<void **>(&p->tvals), b), "hipMalloc(tvals)");
-                p->dev_bytes += b;
-            }
+            if (!rc) rc = setup_bind(p, C.tsrc, {}, runs, -0.0);
         }
     }
     if (rc) {
@@ -2175,7 +2287,19 @@ SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, voi
     SMFV_REQUIRE(d_values || plan->nnz == 0, "null values");
     hipStream_t st = as_stream(stream);
     const int64_t cnt = plan->snapshot;
-    if (cnt > 0) {
+    if (plan->bind_desc) {
+        // (r4) real entries only, from the descriptors (pads were written at creation)
+        if (plan->nbind_quads > 0) {
+            hipLaunchKernelGGL(k_bind_quads, dim3((unsigned)((plan->nbind_quads + 3) / 4)), dim3(256), 0, st,
+                               plan->nbind_quads, plan->bind_quads, d_values, plan->tvals);
+            SMFV_LAUNCHED();
+        }
+        if (plan->nbind_runs > 0) {
+            hipLaunchKernelGGL(k_bind_runs, dim3((unsigned)plan->nbind_runs), dim3(256), 0, st, plan->bind_runs,
+                               d_values, plan->tvals);
+            SMFV_LAUNCHED();
+        }
+    } else if (cnt > 0) {
         hipLaunchKernelGGL(k_gather_vals, dim3((unsigned)((cnt + 255) / 256)), dim3(256), 0, st, cnt, plan->tsrc,
                            d_values, plan->tvals, plan->mfma ? 0.0 : -0.0);
         SMFV_LAUNCHED();
@@ -2225,6 +2349,7 @@ SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS])
     out[13] = !plan->tiled ? 0.0 : plan->cs ? 4.0 : plan->k1 ? 3.0 : plan->mfma ? 2.0 : 1.0;
     out[14] = plan->cs_chunks;
     out[15] = plan->tiled && !plan->cs && !plan->k1 && !plan->mfma ? plan->ws_geom : 0;
+    out[16] = plan->bind_desc ? 1.0 : 0.0;
     return SMFV_OK;
 }
 

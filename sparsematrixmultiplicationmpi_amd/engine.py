@@ -118,7 +118,7 @@ def _check_dense(T: torch.Tensor, rows: int, K: int, name: str) -> int:
 PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA, PLAN_NATURAL_SEEDS, PLAN_MFMA, PLAN_SPLIT_ENDS = 1, 2, 4, 8, 16, 32
 PLAN_ONE_WAVEFRONT, PLAN_SIMPLE_ROWS, PLAN_CS, PLAN_WS = 64, 128, 256, 512
 PLAN_WS_GEOM1, PLAN_WS_GEOM2, PLAN_WS_GEOM3 = 1024, 2048, 4096
-PLAN_STATS = 16  # SMFV_PLAN_STATS
+PLAN_STATS = 17  # SMFV_PLAN_STATS
 PLAN_KERNELS = {0: None, 1: "k_rows_ws", 2: "k_rows_mfma", 3: "k_spmv_chunks", 4: "k_rows_cs"}
 
 
@@ -185,7 +185,7 @@ class SpmmPlan:
                 "row_begin": int(out[6]), "est_reuse": float(out[7]), "analysis_ms": float(out[8]),
                 "snapshot_entries": int(out[9]), "mfma": bool(out[10]), "xcd_parts": int(out[11]),
                 "footprint": float(out[12]), "kernel": PLAN_KERNELS.get(int(out[13])), "chunks": int(out[14]),
-                "ws_geom": int(out[15])}
+                "ws_geom": int(out[15]), "bind_descriptors": bool(out[16])}
 
     def run(self, X: torch.Tensor, Y: torch.Tensor, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
         A, K = self.A, self.K
