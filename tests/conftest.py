@@ -31,6 +31,45 @@ def load_golden(name):
     return dict(np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False))
 
 
+def golden_large_cases():
+    """(r4) The fixtures at SURVEY 8(c)'s sizes (tests/golden/make_golden_large.py)."""
+    import json
+    with open(os.path.join(GOLDEN, "manifest_large.json")) as f:
+        return json.load(f)
+
+
+def load_golden_large(name):
+    """A large fixture: the CSR its compact inputs stand for (values k / 7),
+    and the reference's result hashes / NonZeroElement XOR masks."""
+    import numpy as np
+    from sparsematrixmultiplicationmpi_amd import inputs
+    g = dict(np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False))
+    m, n = int(g["m"]), int(g["n"])
+    rp = np.zeros(m + 1, np.int32)
+    rp[1:] = np.cumsum(g["lens"].astype(np.int64))
+    row = np.repeat(np.arange(m, dtype=np.int64), g["lens"].astype(np.int64))
+    ci = (row + g["off"].astype(np.int64)).astype(np.int32)
+    g["A"] = inputs.SparseMatrix(g["vals"].astype(np.float64) / 7.0, ci, rp, m, n)
+    return g
+
+
+def golden_large_nnz(g, K, p, Y_seq):
+    """The reference's NonZeroElement result at p ranks, rebuilt exactly from
+    its sequential result (checked against sha_seq by the caller) and the
+    fixture's XOR mask."""
+    import numpy as np
+    y = np.ascontiguousarray(Y_seq, dtype=np.float64).copy().reshape(-1).view(np.uint64)
+    idx = g[f"nnzx_idx_k{K}_p{p}"]
+    y[idx] ^= g[f"nnzx_xor_k{K}_p{p}"]
+    return y.view(np.float64).reshape(Y_seq.shape)
+
+
+def sha_f64(a):
+    import hashlib
+    import numpy as np
+    return hashlib.sha256(np.ascontiguousarray(a, dtype=np.float64).tobytes()).hexdigest()
+
+
 @pytest.fixture(scope="session")
 def gpu():
     import torch

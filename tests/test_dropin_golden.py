@@ -42,3 +42,25 @@ def test_dropin_golden(tmp_path, name):
                             str(tmp_path / "x.bin"), str(tmp_path / "y.bin")],
                            capture_output=True, text=True, timeout=120, env=dict(os.environ, **env))
         assert r.returncode == 0 and "DROPIN GOLDEN OK" in r.stdout, (env, r.stdout[-3000:], r.stderr[-3000:])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,K", [("sym2k", 3), ("sym2k", 128), ("plaw20k", 1), ("plaw20k", 32)])
+def test_dropin_golden_large(tmp_path, name, K):
+    """(r4) The same compiled program on the fixtures at SURVEY 8(c)'s sizes:
+    the Y it is checked against is the oracle's, accepted only after its
+    sha256 equals the fixture's hash of the REFERENCE's own sequential bytes."""
+    from conftest import load_golden_large, sha_f64
+    from oracle import oracle
+    g = load_golden_large(name)
+    A = g["A"]
+    X = smfv.generateLargeFatVector(A.numCols, K)
+    Y = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    assert sha_f64(Y) == str(g[f"sha_seq_k{K}"])
+    smfv.inputs.write_csr_bin(str(tmp_path / "a.bin"), A)
+    smfv.inputs.write_dense_bin(str(tmp_path / "x.bin"), X)
+    smfv.inputs.write_dense_bin(str(tmp_path / "y.bin"), Y)
+    r = subprocess.run([MPIEXEC, "-launcher", "fork", "-n", "1", PROG, str(tmp_path / "a.bin"),
+                        str(tmp_path / "x.bin"), str(tmp_path / "y.bin")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "DROPIN GOLDEN OK" in r.stdout, (r.stdout[-3000:], r.stderr[-3000:])

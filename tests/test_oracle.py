@@ -114,3 +114,48 @@ def test_mtx_errors(tmp_path):
     bad.write_text("%%MatrixMarket matrix coordinate real general\n2 2 3\n1 1 1.0\n")
     with pytest.raises(ValueError):
         oracle.mtx_read(str(bad))
+
+
+# ---- (r4) fixtures at SURVEY 8(c)'s sizes (tests/golden/make_golden_large.py) ----
+from conftest import golden_large_cases, golden_large_nnz, load_golden_large, sha_f64  # noqa: E402
+
+LARGE = sorted(golden_large_cases())
+
+
+def test_large_manifest_hashes_and_sizes():
+    for name, info in golden_large_cases().items():
+        with open(os.path.join(GOLDEN, f"{name}.npz"), "rb") as f:
+            b = f.read()
+        assert hashlib.sha256(b).hexdigest() == info["sha256"], name
+        assert len(b) < 1 << 20, name  # each under 1 MB
+        A = load_golden_large(name)["A"]
+        assert hashlib.sha256(A.rowPtr.tobytes() + A.colIndices.tobytes() + A.values.tobytes()).hexdigest() == \
+            info["a_sha"], name
+
+
+@pytest.mark.parametrize("name", LARGE)
+def test_large_oracle_vs_reference(name):
+    """The oracle against the reference's own results at 2k / 20k rows, K in
+    {1, 3, 32, 128}, p in {1, 2, 3, 8}: sequential / RowWise / ColumnWise by
+    the sha256 of the reference's bytes; NonZeroElement bitwise at p <= 2 and
+    within 1e-12 x sum|a||x| beyond (the MPICH reduce association)."""
+    g = load_golden_large(name)
+    info = golden_large_cases()[name]
+    A = g["A"]
+    for K in info["K"]:
+        X = oracle.fatvector_rand(A.numCols, K)  # the reference driver's X
+        assert sha_f64(X) == info[f"x_sha_k{K}"]
+        Y = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+        assert sha_f64(Y) == str(g[f"sha_seq_k{K}"]), (name, K)
+        absY = oracle.spmm("sequential", A.rowPtr, A.colIndices, np.abs(A.values), X)
+        for p in info["p"]:
+            assert sha_f64(oracle.spmm("rowwise", A.rowPtr, A.colIndices, A.values, X, p)) == \
+                str(g[f"sha_row_k{K}_p{p}"]), (name, K, p)
+            assert sha_f64(oracle.spmm("columnwise", A.rowPtr, A.colIndices, A.values, X, p)) == \
+                str(g[f"sha_col_k{K}_p{p}"]), (name, K, p)
+            ref = golden_large_nnz(g, K, p, Y)
+            Yz = oracle.spmm("nonzero", A.rowPtr, A.colIndices, A.values, X, p)
+            if p <= 2:
+                assert np.array_equal(Yz.view(np.uint64), ref.view(np.uint64)), (name, K, p)
+            else:
+                assert oracle.max_rel_err(Yz, ref, absY) <= 1e-12, (name, K, p)
