@@ -149,6 +149,9 @@ def build_matrix(kind: str, mtx: str | None):
 # ---------------------------------------------------------------------------
 # CPU baseline (reference RowWise under MPI on the host cores)
 # ---------------------------------------------------------------------------
+MPI_BIND = ["-bind-to", "core"]  # (r4) one rank per core, stated in cpu_baseline.binding
+
+
 def _ref_run(A, K: int, tag: str, cores: int, binary: str, reps: int, timeout: float) -> float | None:
     """One timed run of the reference's compiled sources (oracle/_ref) under
     MPICH: seconds per call of variant `tag`, as SC/main.cpp:161-163 times it."""
@@ -157,12 +160,21 @@ def _ref_run(A, K: int, tag: str, cores: int, binary: str, reps: int, timeout: f
     with tempfile.TemporaryDirectory() as tmp:
         csr = os.path.join(tmp, "a.bin")
         inputs.write_csr_bin(csr, A)
-        cmd = [MPIEXEC, "-launcher", "fork", "-n", str(cores), binary, csr, str(K), "--reps", str(reps),
-               "--variants", tag]
+        cmd = [MPIEXEC, "-launcher", "fork"] + MPI_BIND + ["-n", str(cores), binary, csr, str(K), "--reps",
+                                                            str(reps), "--variants", tag]
+        # own process group: on a timeout mpiexec AND its ranks are killed
+        proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                                start_new_session=True)
         try:
-            out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, check=True).stdout
-        except (subprocess.SubprocessError, OSError) as e:
-            print(f"[bench] reference CPU run failed ({e})", file=sys.stderr)
+            out, err = proc.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            import signal
+            os.killpg(proc.pid, signal.SIGKILL)
+            proc.communicate()
+            print(f"[bench] reference CPU run over {timeout:.0f} s (-n {cores}); killed", file=sys.stderr)
+            return None
+        if proc.returncode != 0:
+            print(f"[bench] reference CPU run failed (rc {proc.returncode}): {err[-300:]}", file=sys.stderr)
             return None
     mt = re.search(rf"{re.escape(name)} Execution time: ([0-9.eE+-]+)", out)
     return float(mt.group(1)) if mt else None
@@ -185,19 +197,30 @@ def cpu_baseline(A, K: int, variant: str, sample: str | None = None, budget_s: f
     what = sample or f"full matrix, K={K}"
     if os.path.exists(ref) and os.path.exists(MPIEXEC):
         t0 = time.time()
-        # 16 = this process's CPU share on the GPU box (gpurun: 16 per GPU)
+        # 16 = this process's CPU share on the GPU box (gpurun: 16 per GPU);
+        # SURVEY 8(d) also asks for -n nproc: run last, capped in time (over
+        # the share it oversubscribes the 16 CPUs; its rate is reported, not used)
+        nproc = os.cpu_count() or 16
         counts = [1] if tag == "S" else ([1, 2, 4, 8, 16] if sweep_ranks else [16])
         sweep = {}
         for c in counts:
             t = _ref_run(A, K, tag, c, ref, 5 if c == counts[-1] and sweep_ranks else 3, budget_s * 6)
             if t:
                 sweep[str(c)] = round(flops / t / 1e9, 4)
+        nproc_point = None
+        if sweep_ranks and tag != "S" and nproc not in counts:
+            t = _ref_run(A, K, tag, nproc, ref, 3, 90.0)
+            nproc_point = {"ranks": nproc, "GFLOPs": round(flops / t / 1e9, 4) if t else None,
+                           "note": "mpiexec -n nproc (SURVEY 8d); nproc counts the whole host, this process's "
+                                   "share is 16 CPUs, so it oversubscribes; None = over its 90 s cap or failed"}
         top = str(counts[-1])
         if top in sweep:
             o0 = (_ref_run(A, K, tag, counts[-1], ref0, 3, budget_s * 6)
                   if os.path.exists(ref0) and sweep_ranks else None)
             return {"value": sweep[top], "unit": "GFLOP/s", "cores": counts[-1], "kind": "reference",
-                    "host_cpus": os.cpu_count(),
+                    "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+                    "binding": "MPICH hydra " + " ".join(MPI_BIND) + " (one rank per core), -launcher fork",
+                    "nproc_point": nproc_point,
                     "sample": f"{what}, reference {name} (SC sources, g++ -O3) under MPICH mpiexec -n {top}, "
                               f"median of {5 if sweep_ranks else 3} calls incl. gather + FatVector rebuild"
                               f"{'; 1/2/4/8/16-rank sweep and the -O0 build beside it' if sweep_ranks else ''}; "
