@@ -27,6 +27,9 @@
 
 // Creates the HIP context on this rank's GPU, loads the library's code
 // object and starts the runtime's host<->device copy path (smfv_device_init).
+// (r4) It also grows the caller's heap once (SMFV_HEAP_PREFAULT_MB, default
+// 96; 0 = off): freed heap stays mapped and that much is faulted in, so the
+// first result FatVectors do not pay a page fault per 4 KiB.
 // Returns its wall time (seconds).  Optional: the first call does
 // it otherwise, inside its own time.
 double smfvInitDevice();
