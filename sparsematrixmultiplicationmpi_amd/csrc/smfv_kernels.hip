@@ -1000,21 +1000,45 @@ __global__ __launch_bounds__(256) void k_gather_vals(int64_t count, const int *_
 // Quad q (WS_QWORDS... expanded to 10 ints on the host: first pair, pairs,
 // then (CSR start, length) of its 4 rows): pair j holds entries 2 (j / 4),
 // +1 of row j % 4.  One wave per quad.
+constexpr int BIND_QPW = 4;  // quads per wave: one round of waves covers the chip's snapshot
 __global__ __launch_bounds__(256) void k_bind_quads(int64_t nq, const int *__restrict__ qd,
                                                     const double *__restrict__ va, double *__restrict__ tv)
 {
-    const int64_t qi = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (qi >= nq) return;
-    const int *d = qd + qi * 10;
-    const int pb = d[0], np = d[1];
-    for (int j = threadIdx.x & 63; j < np; j += 64) {
+    // wave w takes quads [BIND_QPW w, BIND_QPW (w + 1)); the descriptors are
+    // wave-uniform (scalar loads, all issued first), then every lane's value
+    // loads of all its quads go out before any store: 4x the bytes in flight
+    // of one quad per wave, whose descriptor -> values -> store chain left the
+    // bind latency-bound (16.8 us on cop20k)
+    const int64_t q0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * BIND_QPW;
+    if (q0 >= nq) return;
+    const int lane = threadIdx.x & 63;
+    int d[BIND_QPW][10];
+#pragma unroll
+    for (int u = 0; u < BIND_QPW; ++u)
+#pragma unroll
+        for (int f = 0; f < 10; ++f) d[u][f] = q0 + u < nq ? qd[(q0 + u) * 10 + f] : (f == 1 ? 0 : 0);
+    int npmax = 0;
+#pragma unroll
+    for (int u = 0; u < BIND_QPW; ++u) npmax = max(npmax, d[u][1]);
+    for (int j = lane; j < npmax; j += 64) {
         const int k = j & 3, el = (j >> 2) * 2;
-        const int src = d[2 + 2 * k], len = d[3 + 2 * k];
-        double *o = tv + 2 * ((int64_t)pb + j);
-        if (el + 1 < len)
-            *reinterpret_cast<ws::d2 *>(o) = ws::d2{va[src + el], va[src + el + 1]};
-        else if (el < len)
-            o[0] = va[src + el];
+        double a[BIND_QPW], b[BIND_QPW];
+#pragma unroll
+        for (int u = 0; u < BIND_QPW; ++u) {
+            const int src = d[u][2 + 2 * k], len = d[u][3 + 2 * k];
+            a[u] = j < d[u][1] && el < len ? va[src + el] : 0.0;
+            b[u] = j < d[u][1] && el + 1 < len ? va[src + el + 1] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < BIND_QPW; ++u) {
+            const int len = d[u][3 + 2 * k];
+            if (j >= d[u][1] || el >= len) continue;
+            double *o = tv + 2 * ((int64_t)d[u][0] + j);
+            if (el + 1 < len)
+                *reinterpret_cast<ws::d2 *>(o) = ws::d2{a[u], b[u]};
+            else
+                o[0] = a[u];
+        }
     }
 }
 // contiguous runs (direct rows, K = 1 chunks): {dst entry, src, count}, one block per run
@@ -2290,7 +2314,8 @@ SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, voi
     if (plan->bind_desc) {
         // (r4) real entries only, from the descriptors (pads were written at creation)
         if (plan->nbind_quads > 0) {
-            hipLaunchKernelGGL(k_bind_quads, dim3((unsigned)((plan->nbind_quads + 3) / 4)), dim3(256), 0, st,
+            const int64_t waves = (plan->nbind_quads + BIND_QPW - 1) / BIND_QPW;
+            hipLaunchKernelGGL(k_bind_quads, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st,
                                plan->nbind_quads, plan->bind_quads, d_values, plan->tvals);
             SMFV_LAUNCHED();
         }

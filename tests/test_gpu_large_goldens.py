@@ -5,9 +5,9 @@ and has direct rows, at K in {1, 3, 32, 128} and p in {1, 2, 3, 8}, with the
 reference's X (rand()%100+1).
 
   one device   every variant's default plan (tiled where it pays, the K = 1
-               chunk plan, the merge path with tiles off) -> the sha256 of the
-               reference's sequential bytes (NONZERO's merge path: within
-               1e-12 x sum|a||x| of the reference's NonZeroElement at p = 1)
+               chunk plan) -> the sha256 of the reference's sequential bytes;
+               NONZERO on the merge path (untiled K, or tiles off): within
+               1e-12 x sum|a||x| of the reference's NonZeroElement at p = 1
   p ranks      every rank plan (smfv_dist_plan_create_rank), the shares moved
                as the native exchange schedule says and assembled on the
                device -> the sha256 of the reference's RowWise / ColumnWise
@@ -65,7 +65,12 @@ def test_one_device_vs_reference(gpu, problems, name, K):
         Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
         plan.run(dX, Y)
         torch.cuda.synchronize()
-        assert sha_f64(Y.cpu().numpy()) == sha, (name, K, v)
+        if v == smfv.Variant.NONZERO and not st["tiled"]:
+            # untiled NONZERO (K not a multiple of 32, no K = 1 chunk plan) is
+            # the nnz-balanced merge path: reassociated, within tolerance
+            assert rel(Y.cpu().numpy(), golden_large_nnz(g, K, 1, Yseq), absY) <= NNZ_TOL, (name, K)
+        else:
+            assert sha_f64(Y.cpu().numpy()) == sha, (name, K, v, st["tiled"])
     Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
     smfv.SpmmPlan(smfv.Variant.NONZERO, dA, K, tiles="off").run(dX, Y)
     torch.cuda.synchronize()
