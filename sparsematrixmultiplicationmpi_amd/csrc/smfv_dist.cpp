@@ -499,8 +499,10 @@ static int dist_plan_create(smfv_dist_plan_t *out, smfv_comm_t comm, int p, int 
         default: {  // nnz range [s, e) over rows [f, l] (SC/...NonZeroElement.cpp:24-67)
             int64_t s, e;
             smfv_partition_nnz(nnz, p, rank, &s, &e);
-            rc = smfv::plan_create(&d->local, SMFV_NONZERO, f, std::max(0, l - f + 1), n, s, e, nullptr, nullptr, K,
-                                   flags, f);
+            // (r4) the pattern is passed: the range's whole rows take a row-block
+            // plan, the cut rows the merge path (smfv::plan_create)
+            rc = smfv::plan_create(&d->local, SMFV_NONZERO, f, std::max(0, l - f + 1), n, s, e, h_row_ptr, h_col_idx,
+                                   K, flags, f);
         }
         }
     }

@@ -358,6 +358,85 @@ __global__ __launch_bounds__(NT) void k_spmv_chunks(const int4 *__restrict__ hdr
 #endif
 
 // ---------------------------------------------------------------------------
+// (r4) k_panel_chunks: the same chunk plan for a narrow panel, 1 < kc < 32
+// columns (SC/...ColumnWise.cpp:34-48: a rank's K/p column window, and any
+// one-device K below the tiled kernel's 32-column panel).  The chunk's
+// entries (values snapshot, 16-bit column offsets) are loaded once; for each
+// group of CG columns every entry gathers its CG X values from the window
+// and its CG products go to LDS (the partial accumulators), then lane t sums
+// row t's products column by column in CSR order (separate multiply and
+// add: bit-identical) and stores CG contiguous doubles of the panel row.
+// One pass over the CSR whatever kc (the untiled row kernel re-streamed it
+// at 1.4 TB/s with 2-lane rows).
+// ---------------------------------------------------------------------------
+template <int NT, int CH, bool WIDE, int CG>
+__global__ __launch_bounds__(NT) void k_panel_chunks(const int4 *__restrict__ hdr, const uint16_t *__restrict__ rs,
+                                                     const uint16_t *__restrict__ off, const int *__restrict__ col,
+                                                     const double *__restrict__ vals,
+                                                     const double *__restrict__ X, int64_t ldx, int kc,
+                                                     double *__restrict__ Y, int64_t ldy)
+{
+    static_assert(CH % (2 * NT) == 0, "whole entry pairs per lane");
+    constexpr int V2 = CH / (2 * NT);
+    __shared__ double prod[CH * CG];
+    const int c = xcd_remap(blockIdx.x, gridDim.x);
+    const int t = threadIdx.x;
+    const int4 h = hdr[c];  // first row, rows, base column, entries
+    const chunk_d2 *v2 = reinterpret_cast<const chunk_d2 *>(vals + (int64_t)c * CH);
+    const uint32_t *o2 = reinterpret_cast<const uint32_t *>(off + (int64_t)c * CH);
+    const uint64_t *c2 = reinterpret_cast<const uint64_t *>(col + (int64_t)c * CH);
+    chunk_d2 v[V2];
+    int64_t j0[V2], j1[V2];
+#pragma unroll
+    for (int k = 0; k < V2; ++k) {
+        v[k] = __builtin_nontemporal_load(v2 + k * NT + t);
+        if constexpr (WIDE) {
+            const uint64_t cc = __builtin_nontemporal_load(c2 + k * NT + t);
+            j0[k] = (int64_t)(int)(uint32_t)cc;
+            j1[k] = (int64_t)(int)(uint32_t)(cc >> 32);
+        } else {
+            const uint32_t o = __builtin_nontemporal_load(o2 + k * NT + t);
+            j0[k] = (int64_t)(o & 0xFFFFu);
+            j1[k] = (int64_t)(o >> 16);
+        }
+    }
+    const uint16_t *rsc = rs + (int64_t)c * (NT + 1);
+    const int a = rsc[t], b = rsc[t + 1];
+    const double *xb = X + (int64_t)h.z * ldx;
+    for (int c0 = 0; c0 < kc; c0 += CG) {
+#pragma unroll
+        for (int k = 0; k < V2; ++k) {
+            const int e0 = 2 * (k * NT + t);
+            double x0[CG], x1[CG];
+#pragma unroll
+            for (int q = 0; q < CG; ++q) {  // pads and columns past kc gather nothing
+                x0[q] = e0 < h.w && c0 + q < kc ? xb[j0[k] * ldx + c0 + q] : 0.0;
+                x1[q] = e0 + 1 < h.w && c0 + q < kc ? xb[j1[k] * ldx + c0 + q] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < CG; ++q) {
+                prod[e0 * CG + q] = v[k].x * x0[q];
+                prod[(e0 + 1) * CG + q] = v[k].y * x1[q];
+            }
+        }
+        __syncthreads();
+        if (t < h.y) {
+            double acc[CG];
+#pragma unroll
+            for (int q = 0; q < CG; ++q) acc[q] = 0.0;
+            for (int j = a; j < b; ++j)
+#pragma unroll
+                for (int q = 0; q < CG; ++q) acc[q] = acc[q] + prod[j * CG + q];
+            double *y = Y + (int64_t)(h.x + t) * ldy + c0;
+#pragma unroll
+            for (int q = 0; q < CG; ++q)
+                if (c0 + q < kc) y[q] = acc[q];
+        }
+        __syncthreads();  // the products' LDS is rewritten by the next column group
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_rows_mh: the production row kernel for K even and 16-byte aligned X/Y.
 //
 //  * a block of 256 lanes owns 256/TEAM consecutive rows; it stages its
@@ -995,51 +1074,29 @@ __global__ __launch_bounds__(256) void k_gather_vals(int64_t count, const int *_
 
 // (r4) The bind from descriptors: only the real entries of the snapshot are
 // written (its pads were filled once at plan creation, k_fill_f64), and the
-// sources come from per-quad / per-run descriptors instead of a per-entry
-// int32 index: 16 B moved per non-zero instead of 28 per snapshot entry.
-// Quad q (WS_QWORDS... expanded to 10 ints on the host: first pair, pairs,
-// then (CSR start, length) of its 4 rows): pair j holds entries 2 (j / 4),
-// +1 of row j % 4.  One wave per quad.
-constexpr int BIND_QPW = 4;  // quads per wave: one round of waves covers the chip's snapshot
-__global__ __launch_bounds__(256) void k_bind_quads(int64_t nq, const int *__restrict__ qd,
+// sources come from a per-PAIR table (4 B per 16-B value pair, instead of a
+// 4-B index per 8-B entry): pt[i] = CSR index of pair i's first value when
+// both are real, -(index + 2) when only the first is, -1 for a pad pair.  A
+// lane binds two pairs (one 8-B table load, four value loads, two stores).
+// Tiles' pairs interleave the 4 rows of a quad, so a wave's value loads are
+// 4 runs of 256 contiguous bytes.
+__global__ __launch_bounds__(256) void k_bind_pairs(int64_t npairs, const int2 *__restrict__ pt,
                                                     const double *__restrict__ va, double *__restrict__ tv)
 {
-    // wave w takes quads [BIND_QPW w, BIND_QPW (w + 1)); the descriptors are
-    // wave-uniform (scalar loads, all issued first), then every lane's value
-    // loads of all its quads go out before any store: 4x the bytes in flight
-    // of one quad per wave, whose descriptor -> values -> store chain left the
-    // bind latency-bound (16.8 us on cop20k)
-    const int64_t q0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * BIND_QPW;
-    if (q0 >= nq) return;
-    const int lane = threadIdx.x & 63;
-    int d[BIND_QPW][10];
-#pragma unroll
-    for (int u = 0; u < BIND_QPW; ++u)
-#pragma unroll
-        for (int f = 0; f < 10; ++f) d[u][f] = q0 + u < nq ? qd[(q0 + u) * 10 + f] : (f == 1 ? 0 : 0);
-    int npmax = 0;
-#pragma unroll
-    for (int u = 0; u < BIND_QPW; ++u) npmax = max(npmax, d[u][1]);
-    for (int j = lane; j < npmax; j += 64) {
-        const int k = j & 3, el = (j >> 2) * 2;
-        double a[BIND_QPW], b[BIND_QPW];
-#pragma unroll
-        for (int u = 0; u < BIND_QPW; ++u) {
-            const int src = d[u][2 + 2 * k], len = d[u][3 + 2 * k];
-            a[u] = j < d[u][1] && el < len ? va[src + el] : 0.0;
-            b[u] = j < d[u][1] && el + 1 < len ? va[src + el + 1] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < BIND_QPW; ++u) {
-            const int len = d[u][3 + 2 * k];
-            if (j >= d[u][1] || el >= len) continue;
-            double *o = tv + 2 * ((int64_t)d[u][0] + j);
-            if (el + 1 < len)
-                *reinterpret_cast<ws::d2 *>(o) = ws::d2{a[u], b[u]};
-            else
-                o[0] = a[u];
-        }
-    }
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // pairs 2i, 2i + 1
+    if (2 * i >= npairs) return;
+    const int2 d = 2 * i + 1 < npairs ? pt[i] : int2{reinterpret_cast<const int *>(pt)[2 * i], -1};
+    ws::d2 *o = reinterpret_cast<ws::d2 *>(tv) + 2 * i;
+    const int s0 = d.x >= 0 ? d.x : -d.x - 2, s1 = d.y >= 0 ? d.y : -d.y - 2;
+    double a0 = 0.0, b0 = 0.0, a1 = 0.0, b1 = 0.0;
+    if (d.x != -1) a0 = va[s0];
+    if (d.x >= 0) b0 = va[s0 + 1];
+    if (d.y != -1) a1 = va[s1];
+    if (d.y >= 0) b1 = va[s1 + 1];
+    if (d.x >= 0) o[0] = ws::d2{a0, b0};
+    else if (d.x != -1) reinterpret_cast<double *>(o)[0] = a0;
+    if (d.y >= 0) o[1] = ws::d2{a1, b1};
+    else if (d.y != -1) reinterpret_cast<double *>(o + 1)[0] = a1;
 }
 // contiguous runs (direct rows, K = 1 chunks): {dst entry, src, count}, one block per run
 __global__ __launch_bounds__(256) void k_bind_runs(const int64_t *__restrict__ rd, const double *__restrict__ va,
@@ -1049,6 +1106,46 @@ __global__ __launch_bounds__(256) void k_bind_runs(const int64_t *__restrict__ r
     const int64_t dst = d[0], src = d[1], cnt = d[2];
     for (int64_t i = threadIdx.x; i < cnt; i += 256) tv[dst + i] = va[src + i];
 }
+// (r4) The cut rows of a NONZERO range (at most its first and last row):
+// row i's partial sum over its entries [s[i], e[i]), one block per row.
+// With K <= 256 the block's lanes are G = 256 / K groups of K columns; group g
+// sums entries s + g, s + g + G, ... and the G partials are added in group
+// order (deterministic; within the NonZeroElement tolerance, like the merge
+// path it replaces for these rows).  K > 256: one group, columns looped.
+struct CutRows {
+    int n, row[2];
+    int64_t s[2], e[2];
+    int64_t yoff[2];  // the row's offset in Y (doubles)
+};
+__global__ __launch_bounds__(256) void k_cut_rows(CutRows cr, const int *__restrict__ ci, const double *__restrict__ va,
+                                                  const double *__restrict__ X, int64_t ldx, int K,
+                                                  double *__restrict__ Y)
+{
+    __shared__ double part[256];
+    const int i = blockIdx.x, t = threadIdx.x;
+    const int64_t s = cr.s[i], e = cr.e[i];
+    double *y = Y + cr.yoff[i];
+    if (K > 256) {
+        for (int c = t; c < K; c += 256) {
+            double acc = 0.0;
+            for (int64_t j = s; j < e; ++j) acc = acc + va[j] * X[(int64_t)ci[j] * ldx + c];
+            y[c] = acc;
+        }
+        return;
+    }
+    const int G = 256 / K, g = t / K, c = t % K;
+    double acc = 0.0;
+    if (g < G)
+        for (int64_t j = s + g; j < e; j += G) acc = acc + va[j] * X[(int64_t)ci[j] * ldx + c];
+    part[t] = acc;
+    __syncthreads();
+    if (t < K) {
+        double sum = 0.0;
+        for (int q = 0; q < G; ++q) sum = sum + part[q * K + t];
+        y[t] = sum;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_fill_f64(int64_t n, double v, double *__restrict__ out)
 {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) out[i] = v;
@@ -1767,9 +1864,9 @@ struct smfv_plan_s {
     int parts = 1;                 // 8: one part of the rows per XCD (build_ws_plan)
     double footprint = -1.0;       // parts_footprint of the 8 parts
     int *tsrc = nullptr;                   // snapshot entry -> CSR index of its value (-1: pad); NULL with descriptors
-    int *bind_quads = nullptr;             // (r4) bind descriptors: 10 ints per quad (k_bind_quads)
+    int *bind_pairs = nullptr;             // (r4) bind descriptors: one int per value pair (k_bind_pairs)
     int64_t *bind_runs = nullptr;          // (r4) 3 int64 per contiguous run (k_bind_runs)
-    int64_t nbind_quads = 0, nbind_runs = 0;
+    int64_t nbind_pairs = 0, nbind_runs = 0;
     bool bind_desc = false;                // bind from the descriptors (pads filled at creation)
     double *tvals = nullptr;               // the bound values snapshot (tile order, pads -0.0, then direct rows)
     const double *bound_values = nullptr;  // d_values the snapshot came from
@@ -1794,9 +1891,17 @@ struct smfv_plan_s {
     size_t ws_bytes = 0, dev_bytes = 0;
     hipEvent_t bind_ev = nullptr;          // recorded after the snapshot gather
     hipStream_t bind_stream = nullptr;
+    // (r4) NONZERO over an nnz range that cuts rows (a rank's share): the
+    // range's whole rows as a row-block plan (tiled / chunked), the cut first
+    // and last rows on the merge path
+    smfv_plan_s *sub = nullptr;
+    int sub_row = 0;                       // the sub-plan's first row, block-local
+    int ncut = 0, cut_row[2] = {0, 0};     // cut rows (global) and their nnz ranges
+    int64_t cut_s[2] = {0, 0}, cut_e[2] = {0, 0};
     ~smfv_plan_s()
     {
-        for (void *q : {(void *)tsrc, (void *)bind_quads, (void *)bind_runs, (void *)tvals, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
+        delete sub;
+        for (void *q : {(void *)tsrc, (void *)bind_pairs, (void *)bind_runs, (void *)tvals, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
                         (void *)direct_off, (void *)ws_loff, ws, (void *)mf_rec, (void *)mf_ucols, (void *)mf_bstep,
                         (void *)k1_hdr, (void *)k1_rs, (void *)k1_off, (void *)k1_col, (void *)cs_bs,
                         (void *)cs_trow, (void *)cs_tlast, (void *)cs_crec, (void *)cs_aux})
@@ -1817,28 +1922,25 @@ template <class T> int upload(T **dst, const std::vector<T> &src, size_t &acc)
 
 }  // namespace
 
-// (r4) The snapshot's sources as bind descriptors (quads of the tiled layout,
-// contiguous runs), checked on the host against the per-entry sources `ts`
-// (each real entry once, from the same CSR index; pads untouched).  On a
-// match the descriptors are uploaded and the pads written once; otherwise
-// the plan keeps the per-entry gather (k_gather_vals over ts).
-static int setup_bind(smfv_plan_s *p, const std::vector<int> &ts, const std::vector<int> &quads,
+// (r4) The snapshot's sources as bind descriptors: a per-pair table for the
+// tiles' pairs [0, npairs) (k_bind_pairs) and contiguous runs for the rest
+// (direct rows, K = 1 chunks; k_bind_runs), checked on the host against the
+// per-entry sources `ts` (each real entry written once, from the same CSR
+// index; pads untouched).  On a match the descriptors are uploaded and the
+// pads written once; otherwise the plan keeps the per-entry gather.
+static int setup_bind(smfv_plan_s *p, const std::vector<int> &ts, const std::vector<int> &pairs,
                       const std::vector<int64_t> &runs, double pad)
 {
     const int64_t n = (int64_t)ts.size();
     std::vector<int> chk((size_t)n, -1);
-    bool ok = true;
-    for (size_t q = 0; ok && q < quads.size() / 10; ++q) {
-        const int *d = &quads[q * 10];
-        for (int j = 0; ok && j < d[1]; ++j) {
-            const int k = j & 3, el = (j >> 2) * 2;
-            for (int h = 0; h < 2 && ok; ++h)
-                if (el + h < d[3 + 2 * k]) {
-                    const int64_t e = 2 * ((int64_t)d[0] + j) + h;
-                    ok = e < n && chk[(size_t)e] == -1;
-                    if (ok) chk[(size_t)e] = d[2 + 2 * k] + el + h;
-                }
-        }
+    bool ok = 2 * (int64_t)pairs.size() <= n;
+    for (size_t i = 0; ok && i < pairs.size(); ++i) {
+        const int d = pairs[i];
+        if (d == -1) continue;
+        const int64_t src = d >= 0 ? d : -(int64_t)d - 2;
+        ok = src >= 0 && chk[2 * i] == -1;
+        if (ok) chk[2 * i] = (int)src;
+        if (ok && d >= 0) chk[2 * i + 1] = (int)(src + 1);
     }
     for (size_t r = 0; ok && r < runs.size() / 3; ++r)
         for (int64_t i = 0; ok && i < runs[3 * r + 2]; ++i) {
@@ -1850,9 +1952,9 @@ static int setup_bind(smfv_plan_s *p, const std::vector<int> &ts, const std::vec
     int rc = SMFV_OK;
     if (ok) {
         p->bind_desc = true;
-        p->nbind_quads = (int64_t)quads.size() / 10;
+        p->nbind_pairs = (int64_t)pairs.size();
         p->nbind_runs = (int64_t)runs.size() / 3;
-        rc = upload(&p->bind_quads, quads, p->dev_bytes);
+        rc = upload(&p->bind_pairs, pairs, p->dev_bytes);
         if (!rc) rc = upload(&p->bind_runs, runs, p->dev_bytes);
     } else {
         rc = upload(&p->tsrc, ts, p->dev_bytes);
@@ -2024,7 +2126,30 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
             std::string err;
             // a pattern the tile layout cannot take (the replayed plan fails its
             // checks) keeps the untiled plan rather than failing the create
-            if (build_ws_plan(m, n, rpl.data(), cil, W, &err, caps)) {
+            bool built = build_ws_plan(m, n, rpl.data(), cil, W, &err, caps);
+            // (r4) a small plan (a rank's row block at p = 8: ~1 tile per CU
+            // with 64-row tiles, one unit per block, all fill and drain) takes
+            // geometry 2 unless the caller chose one: half-size tiles, two
+            // blocks per CU (p = 8 on cop20k: 7.9 -> 7.1 us; at ~2 tiles per
+            // CU, p = 4, geometry 1 stays ahead)
+            if (built && W.ntiles > 0 &&
+                !(flags & (SMFV_PLAN_WS_GEOM1 | SMFV_PLAN_WS_GEOM2 | SMFV_PLAN_WS_GEOM3))) {
+                int dev = 0, ncu = 256;
+                if (hipGetDevice(&dev) == hipSuccess) {
+                    int v = 0;
+                    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+                        ncu = v;
+                }
+                if (2 * W.ntiles < 3 * ncu) {
+                    TileCaps c2 = plan_caps(flags | SMFV_PLAN_WS_GEOM2, col_base);
+                    c2.part_rows = caps.part_rows;
+                    c2.part_start = caps.part_start;
+                    WsPlan W2;
+                    std::string err2;
+                    if (build_ws_plan(m, n, rpl.data(), cil, W2, &err2, c2)) W = std::move(W2);
+                }
+            }
+            if (built) {
                 p->ws_geom = W.geom.id;
                 p->ntiles = W.ntiles;
                 for (int x = 0; x <= 8; ++x) p->ws_xcd[x] = W.xcd[x];
@@ -2047,17 +2172,12 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                         for (int j = rpl[r]; j < rpl[r + 1]; ++j) ts.push_back((int)(nnz_base + j));
                     }
                     p->snapshot = (int64_t)ts.size();
-                    // bind descriptors: the quads (CSR start and length of their rows), the direct rows
-                    std::vector<int> qd;
-                    qd.reserve(W.quads.size() / WS_QWORDS * 10);
-                    for (size_t q = 0; q < W.quads.size(); q += WS_QWORDS) {
-                        qd.push_back(W.quads[q]);
-                        qd.push_back(W.quads[q + 1]);
-                        for (int k = 0; k < 4; ++k) {
-                            const int r = W.quads[q + 2 + k];
-                            qd.push_back(r >= 0 ? (int)(nnz_base + rpl[r]) : 0);
-                            qd.push_back(r >= 0 ? rpl[r + 1] - rpl[r] : 0);
-                        }
+                    // bind descriptors: the tiles' value pairs (from the per-entry
+                    // sources: a pair is two consecutive entries of one row), the direct rows
+                    std::vector<int> pt((size_t)(W.ventries / 2));
+                    for (size_t i = 0; i < pt.size(); ++i) {
+                        const int a = ts[2 * i], b = ts[2 * i + 1];
+                        pt[i] = a < 0 ? -1 : b == a + 1 ? a : -a - 2;
                     }
                     std::vector<int64_t> runs;
                     for (size_t i = 0; i < W.direct.size(); ++i) {
@@ -2069,7 +2189,7 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                     if (!rc) rc = upload(&p->ws_loff, W.loff, p->dev_bytes);
                     if (!rc) rc = upload(&p->direct_rows, W.direct, p->dev_bytes);
                     if (!rc) rc = upload(&p->direct_off, doff, p->dev_bytes);
-                    if (!rc) rc = setup_bind(p, ts, qd, runs, -0.0);
+                    if (!rc) rc = setup_bind(p, ts, pt, runs, -0.0);
                 }
             }
         }
@@ -2077,7 +2197,10 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
     // K = 1: the chunk plan (k_spmv_chunks) wherever the pattern fits its
     // layout (no row over a chunk, 16-bit column spans); otherwise the plan
     // stays untiled (k_spmv_stream on the live CSR)
-    if (!rc && whole_rows && h_rp && h_ci && m > 0 && K == 1 && !(flags & (SMFV_PLAN_NO_TILES | SMFV_PLAN_MFMA))) {
+    // (r4) and 1 < K < 32: the same layout, run by k_panel_chunks (a
+    // ColumnWise rank's K/p window, or a narrow K on one device)
+    if (!rc && whole_rows && h_rp && h_ci && m > 0 && K >= 1 && K < TILE_KP &&
+        !(flags & (SMFV_PLAN_NO_TILES | SMFV_PLAN_MFMA | SMFV_PLAN_SIMPLE_ROWS))) {
         std::vector<int> rpl((size_t)m + 1);
         for (int i = 0; i <= m; ++i) rpl[i] = (int)(h_rp[row_begin + i] - nnz_base);
         SpmvChunkPlan C;
@@ -2102,6 +2225,36 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
             if (!rc) rc = upload(&p->k1_rs, C.rs, p->dev_bytes);
             if (!rc) rc = C.wide ? upload(&p->k1_col, C.col, p->dev_bytes) : upload(&p->k1_off, C.off, p->dev_bytes);
             if (!rc) rc = setup_bind(p, C.tsrc, {}, runs, -0.0);
+        }
+    }
+    // (r4) NONZERO over a range that cuts rows (SC/...NonZeroElement.cpp:24-67
+    // at p > 1): its whole rows are summed in CSR order by the reference too,
+    // so they run as a row-block plan (the tiled kernel / chunk panels,
+    // bit-identical); only the cut rows' partial sums take the merge path
+    if (!rc && variant == SMFV_NONZERO && !whole_rows && h_rp && h_ci && m > 0 && K > 0 &&
+        !(flags & (SMFV_PLAN_NO_TILES | SMFV_PLAN_MFMA | SMFV_PLAN_SIMPLE_ROWS))) {
+        const int f = row_begin, l = row_begin + m - 1;
+        const int fi = h_rp[f] < nnz_base ? f + 1 : f, li = h_rp[l + 1] > nnz_end ? l - 1 : l;
+        if (li >= fi) {
+            smfv_plan_t sub = nullptr;
+            if (plan_create(&sub, SMFV_ROWWISE, fi, li - fi + 1, n, h_rp[fi], h_rp[li + 1], h_rp, h_ci, K, flags, -1) ==
+                    SMFV_OK &&
+                sub->tiled) {
+                p->sub = sub;
+                p->sub_row = fi - f;
+                if (fi > f) {
+                    p->cut_row[p->ncut] = f;
+                    p->cut_s[p->ncut] = nnz_base;
+                    p->cut_e[p->ncut++] = std::min<int64_t>(nnz_end, h_rp[f + 1]);
+                }
+                if (li < l) {
+                    p->cut_row[p->ncut] = l;
+                    p->cut_s[p->ncut] = std::max<int64_t>(nnz_base, h_rp[l]);
+                    p->cut_e[p->ncut++] = nnz_end;
+                }
+            } else {
+                delete sub;  // no gain: the merge path keeps the whole range
+            }
         }
     }
     if (rc) {
@@ -2307,16 +2460,18 @@ SMFV_API void smfv_set_analysis_threads(int threads) { smfv::analysis_threads = 
 SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, void *stream)
 {
     SMFV_REQUIRE(plan, "null plan");
+    if (plan->sub) return smfv_plan_bind_values(plan->sub, d_values, stream);  // (the cut rows read live values)
     if (!plan->tiled) return SMFV_OK;
     SMFV_REQUIRE(d_values || plan->nnz == 0, "null values");
     hipStream_t st = as_stream(stream);
     const int64_t cnt = plan->snapshot;
     if (plan->bind_desc) {
         // (r4) real entries only, from the descriptors (pads were written at creation)
-        if (plan->nbind_quads > 0) {
-            const int64_t waves = (plan->nbind_quads + BIND_QPW - 1) / BIND_QPW;
-            hipLaunchKernelGGL(k_bind_quads, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st,
-                               plan->nbind_quads, plan->bind_quads, d_values, plan->tvals);
+        if (plan->nbind_pairs > 0) {
+            const int64_t lanes = (plan->nbind_pairs + 1) / 2;
+            hipLaunchKernelGGL(k_bind_pairs, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st,
+                               plan->nbind_pairs, reinterpret_cast<const int2 *>(plan->bind_pairs), d_values,
+                               plan->tvals);
             SMFV_LAUNCHED();
         }
         if (plan->nbind_runs > 0) {
@@ -2358,6 +2513,12 @@ SMFV_API int smfv_plan_destroy(smfv_plan_t plan)
 SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS])
 {
     SMFV_REQUIRE(plan && out, "null argument");
+    if (plan->sub) {  // a NONZERO range: its whole rows' plan describes it
+        smfv_plan_stats(plan->sub, out);
+        out[6] = plan->row_begin;
+        out[8] = plan->analysis_ms;
+        return SMFV_OK;
+    }
     out[0] = plan->tiled ? 1.0 : 0.0;
     out[1] = plan->ntiles;
     out[2] = (double)plan->union_rows;
@@ -2371,7 +2532,7 @@ SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS])
     out[10] = plan->mfma ? 1.0 : 0.0;
     out[11] = plan->parts;
     out[12] = plan->footprint;
-    out[13] = !plan->tiled ? 0.0 : plan->cs ? 4.0 : plan->k1 ? 3.0 : plan->mfma ? 2.0 : 1.0;
+    out[13] = !plan->tiled ? 0.0 : plan->cs ? 4.0 : plan->k1 ? (plan->K > 1 ? 5.0 : 3.0) : plan->mfma ? 2.0 : 1.0;
     out[14] = plan->cs_chunks;
     out[15] = plan->tiled && !plan->cs && !plan->k1 && !plan->mfma ? plan->ws_geom : 0;
     out[16] = plan->bind_desc ? 1.0 : 0.0;
@@ -2389,6 +2550,27 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     SMFV_REQUIRE(d_row_ptr && d_Y, "null row_ptr / Y");
     SMFV_REQUIRE(plan->nnz == 0 || (d_col_idx && d_values && d_X), "null col_idx / values / X");
     hipStream_t st = as_stream(stream);
+    if (plan->sub) {
+        // (r4) the whole rows by their plan, then the cut rows' partial sums
+        // (each alone on the merge path: one row, its part of the range)
+        const int rc = smfv_plan_execute(plan->sub, d_row_ptr, d_col_idx, d_values, d_X, ldx,
+                                         d_Y + (int64_t)plan->sub_row * ldy, ldy, stream);
+        if (rc) return rc;
+        if (plan->ncut > 0) {  // one launch for both cut rows
+            CutRows cr{};
+            cr.n = plan->ncut;
+            for (int i = 0; i < plan->ncut; ++i) {
+                cr.row[i] = plan->cut_row[i];
+                cr.s[i] = plan->cut_s[i];
+                cr.e[i] = plan->cut_e[i];
+                cr.yoff[i] = (int64_t)(plan->cut_row[i] - plan->row_begin) * ldy;
+            }
+            hipLaunchKernelGGL(k_cut_rows, dim3((unsigned)plan->ncut), dim3(256), 0, st, cr, d_col_idx, d_values, d_X,
+                               ldx, K, d_Y);
+            SMFV_LAUNCHED();
+        }
+        return SMFV_OK;
+    }
     if (!plan->tiled || (!plan->k1 && pick_vec(d_X, ldx, d_Y, ldy, K) != 2)) {
         // untiled: the row / merge kernels on the live values
         if (plan->variant == SMFV_NONZERO)
@@ -2413,6 +2595,19 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
                       "capturing; synchronize the bind stream before capture");
             return SMFV_ERR_INVALID;
         }
+    }
+    if (plan->k1 && K > 1) {  // (r4) narrow panel
+        if (plan->ntiles > 0) {
+            auto kern = plan->k1_wide ? (K <= 4 ? k_panel_chunks<K1_NT, 1024, true, 4> : k_panel_chunks<K1_NT, 1024, true, 8>)
+                                      : (K <= 4 ? k_panel_chunks<K1_NT, 1024, false, 4>
+                                                : k_panel_chunks<K1_NT, 1024, false, 8>);
+            SMFV_REQUIRE(plan->k1_cap == 1024, "panel chunks need 1,024-entry chunks");
+            hipLaunchKernelGGL(kern, dim3((unsigned)plan->ntiles), dim3(K1_NT), 0, st,
+                               reinterpret_cast<const int4 *>(plan->k1_hdr), plan->k1_rs, plan->k1_off, plan->k1_col,
+                               plan->tvals, d_X, ldx, K, d_Y, ldy);
+            SMFV_LAUNCHED();
+        }
+        return SMFV_OK;
     }
     if (plan->k1) {
         if (plan->ntiles > 0) {

@@ -563,7 +563,6 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     // one tile into the plan at entry offset noff, record index t (the
     // tiles are independent: run in parallel, each with its own pos stamps)
     std::vector<std::vector<int>> tunion;  // each tile's union rows (filled before the emit)
-    std::vector<int64_t> qoff;  // each tile's first quad in P.quads
     auto emit = [&](const std::vector<int> &R, int64_t noff, int64_t vnoff, int t, std::vector<int> &pos,
                     std::vector<int> &stamp, std::vector<int> &ucols, int64_t &tiled, int64_t &unions) {
         ucols.clear();
@@ -617,12 +616,6 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
                 lrec[NR + slot] = lbase | (len2(r) << 16);
                 lrec[2 * NR + slot] = vbase;
                 tiled += rp[r + 1] - rp[r];
-            }
-            {
-                int *qd = &P.quads[(size_t)((qoff[(size_t)t] + q) * WS_QWORDS)];
-                qd[0] = (int)((vnoff + ev) / 2);
-                qd[1] = (int)(vquad(R, (size_t)(4 * q)) / 2);
-                for (int k = 0; k < 4; ++k) qd[2 + k] = 4 * q + k < (int)R.size() ? R[4 * q + k] : -1;
             }
             e += 32 * nb;
             ev += vquad(R, (size_t)(4 * q));
@@ -732,14 +725,11 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     // tiles emitted in parallel into their own ranges
     const int nt = (int)tiles.size();
     std::vector<int64_t> toff((size_t)nt + 1, 0), tvoff((size_t)nt + 1, 0);
-    qoff.assign((size_t)nt + 1, 0);
     for (int t = 0; t < nt; ++t) {
         by_length(tiles[(size_t)t]);
         toff[(size_t)t + 1] = toff[(size_t)t] + layout(tiles[(size_t)t]);
         tvoff[(size_t)t + 1] = tvoff[(size_t)t] + vlayout(tiles[(size_t)t]);
-        qoff[(size_t)t + 1] = qoff[(size_t)t] + ((int64_t)tiles[(size_t)t].size() + 3) / 4;
     }
-    P.quads.assign((size_t)(qoff[(size_t)nt] * WS_QWORDS), -1);
     P.ntiles = nt;
     P.entries = toff[(size_t)nt];
     P.ventries = tvoff[(size_t)nt];

@@ -45,7 +45,6 @@ constexpr int WS_GWORDS = 352, WS_G_NOFF = 256, WS_G_TN = 272, WS_G_NU = 288, WS
 // waves) + wave
 constexpr int WS_LWORDS = 256;
 constexpr int WS_SLACK = 2048;   // entries past the end (DMA over-read of the last tile)
-constexpr int WS_QWORDS = 6;     // WsPlan::quads ints per quad
 
 // (r4) Geometry of a k_rows_ws launch.  cw compute waves of 8 eight-lane
 // teams (rows per tile = 8 cw), lw loader waves of ppw one-KiB X pieces each
@@ -139,10 +138,6 @@ struct WsPlan {
     std::vector<uint8_t> loff;     // per offset entry: its X row in the LDS image (union position; WS_UCAP: pad)
     std::vector<int> tsrc;         // per value entry: CSR index of its value (-1: pad)
     std::vector<int> direct;       // rows over a cap alone, gathered straight from X
-    // (r4) per quad of every tile, WS_QWORDS ints: its first value pair in the
-    // snapshot, its value pairs, then its 4 rows (-1 none); pair j of a quad
-    // holds entries 2 (j / 4), +1 of row j % 4 (the bind's descriptors)
-    std::vector<int> quads;
     int64_t union_rows = 0;        // X rows staged per 32-column panel
     int64_t tiled_nnz = 0;         // non-zeros in tiles (not direct)
     int64_t entries = 0;           // used length of loff (the vector carries WS_SLACK more)
