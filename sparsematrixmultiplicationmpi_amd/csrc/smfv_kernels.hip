@@ -369,16 +369,19 @@ __global__ __launch_bounds__(NT) void k_spmv_chunks(const int4 *__restrict__ hdr
 // One pass over the CSR whatever kc (the untiled row kernel re-streamed it
 // at 1.4 TB/s with 2-lane rows).
 // ---------------------------------------------------------------------------
-template <int NT, int CH, bool WIDE, int CG>
+template <int NT, int CH, bool WIDE, int CG, bool V2X>
 __global__ __launch_bounds__(NT) void k_panel_chunks(const int4 *__restrict__ hdr, const uint16_t *__restrict__ rs,
                                                      const uint16_t *__restrict__ off, const int *__restrict__ col,
                                                      const double *__restrict__ vals,
                                                      const double *__restrict__ X, int64_t ldx, int kc,
                                                      double *__restrict__ Y, int64_t ldy)
 {
-    static_assert(CH % (2 * NT) == 0, "whole entry pairs per lane");
+    static_assert(CH % (2 * NT) == 0 && CG % 2 == 0, "whole entry pairs per lane, column pairs");
     constexpr int V2 = CH / (2 * NT);
-    __shared__ double prod[CH * CG];
+    // column-major partial products (column q of entry e at q * CH + e): the
+    // row sums' lanes (one row each, rows ~27 entries apart) then read
+    // spread banks; entry-major made them collide
+    __shared__ double prod[CG * CH];
     const int c = xcd_remap(blockIdx.x, gridDim.x);
     const int t = threadIdx.x;
     const int4 h = hdr[c];  // first row, rows, base column, entries
@@ -407,17 +410,26 @@ __global__ __launch_bounds__(NT) void k_panel_chunks(const int4 *__restrict__ hd
 #pragma unroll
         for (int k = 0; k < V2; ++k) {
             const int e0 = 2 * (k * NT + t);
+            const bool in0 = e0 < h.w, in1 = e0 + 1 < h.w;  // pads and columns past kc gather nothing
             double x0[CG], x1[CG];
 #pragma unroll
-            for (int q = 0; q < CG; ++q) {  // pads and columns past kc gather nothing
-                x0[q] = e0 < h.w && c0 + q < kc ? xb[j0[k] * ldx + c0 + q] : 0.0;
-                x1[q] = e0 + 1 < h.w && c0 + q < kc ? xb[j1[k] * ldx + c0 + q] : 0.0;
+            for (int q = 0; q < CG; q += 2) {
+                if constexpr (V2X) {  // kc even, X 16-byte aligned with an even stride: pairs of columns
+                    const chunk_d2 z = {0.0, 0.0};
+                    const chunk_d2 p0 = in0 && c0 + q < kc ? *reinterpret_cast<const chunk_d2 *>(xb + j0[k] * ldx + c0 + q) : z;
+                    const chunk_d2 p1 = in1 && c0 + q < kc ? *reinterpret_cast<const chunk_d2 *>(xb + j1[k] * ldx + c0 + q) : z;
+                    x0[q] = p0.x, x0[q + 1] = p0.y, x1[q] = p1.x, x1[q + 1] = p1.y;
+                } else {
+#pragma unroll
+                    for (int h2 = 0; h2 < 2; ++h2) {
+                        x0[q + h2] = in0 && c0 + q + h2 < kc ? xb[j0[k] * ldx + c0 + q + h2] : 0.0;
+                        x1[q + h2] = in1 && c0 + q + h2 < kc ? xb[j1[k] * ldx + c0 + q + h2] : 0.0;
+                    }
+                }
             }
 #pragma unroll
-            for (int q = 0; q < CG; ++q) {
-                prod[e0 * CG + q] = v[k].x * x0[q];
-                prod[(e0 + 1) * CG + q] = v[k].y * x1[q];
-            }
+            for (int q = 0; q < CG; ++q)
+                reinterpret_cast<chunk_d2 *>(prod + q * CH)[k * NT + t] = chunk_d2{v[k].x * x0[q], v[k].y * x1[q]};
         }
         __syncthreads();
         if (t < h.y) {
@@ -426,7 +438,7 @@ __global__ __launch_bounds__(NT) void k_panel_chunks(const int4 *__restrict__ hd
             for (int q = 0; q < CG; ++q) acc[q] = 0.0;
             for (int j = a; j < b; ++j)
 #pragma unroll
-                for (int q = 0; q < CG; ++q) acc[q] = acc[q] + prod[j * CG + q];
+                for (int q = 0; q < CG; ++q) acc[q] = acc[q] + prod[q * CH + j];
             double *y = Y + (int64_t)(h.x + t) * ldy + c0;
 #pragma unroll
             for (int q = 0; q < CG; ++q)
@@ -2146,7 +2158,11 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                     c2.part_start = caps.part_start;
                     WsPlan W2;
                     std::string err2;
-                    if (build_ws_plan(m, n, rpl.data(), cil, W2, &err2, c2)) W = std::move(W2);
+                    // only where the smaller tiles keep the re-use and add no
+                    // direct rows (rows over geometry 2's 125 X rows stay tiled in 1)
+                    if (build_ws_plan(m, n, rpl.data(), cil, W2, &err2, c2) && W2.direct.size() == W.direct.size() &&
+                        W2.union_rows > 0 && (double)W2.tiled_nnz / (double)W2.union_rows >= SMFV_TILE_MIN_REUSE)
+                        W = std::move(W2);
                 }
             }
             if (built) {
@@ -2598,9 +2614,10 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     }
     if (plan->k1 && K > 1) {  // (r4) narrow panel
         if (plan->ntiles > 0) {
-            auto kern = plan->k1_wide ? (K <= 4 ? k_panel_chunks<K1_NT, 1024, true, 4> : k_panel_chunks<K1_NT, 1024, true, 8>)
-                                      : (K <= 4 ? k_panel_chunks<K1_NT, 1024, false, 4>
-                                                : k_panel_chunks<K1_NT, 1024, false, 8>);
+            const bool v2x = K % 2 == 0 && ldx % 2 == 0 && aligned16(d_X);
+#define PK(W_, G_) (v2x ? k_panel_chunks<K1_NT, 1024, W_, G_, true> : k_panel_chunks<K1_NT, 1024, W_, G_, false>)
+            auto kern = plan->k1_wide ? (K <= 4 ? PK(true, 4) : PK(true, 8)) : (K <= 4 ? PK(false, 4) : PK(false, 8));
+#undef PK
             SMFV_REQUIRE(plan->k1_cap == 1024, "panel chunks need 1,024-entry chunks");
             hipLaunchKernelGGL(kern, dim3((unsigned)plan->ntiles), dim3(K1_NT), 0, st,
                                reinterpret_cast<const int4 *>(plan->k1_hdr), plan->k1_rs, plan->k1_off, plan->k1_col,
