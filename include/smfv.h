@@ -125,10 +125,7 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz,
  * to the reference's NonZeroElement with one rank, which sums every row in
  * CSR order); otherwise, and with SMFV_PLAN_NO_TILES, it runs the merge path.
  * With K == 1 (SpMV) a plan over whole rows takes the chunk layout of
- * k_spmv_chunks wherever the pattern fits it (smfv_spmv_chunks_analyse);
- * (r4) so does 1 < K < 32 (k_panel_chunks: the entries loaded once, their
- * products for groups of 4 or 8 columns in LDS, each row summed in CSR order
- * -- a ColumnWise rank's K/p window takes it):
+ * k_spmv_chunks wherever the pattern fits it (smfv_spmv_chunks_analyse):
  * consecutive rows packed into 1,024-entry chunks at fixed addresses, the
  * values snapshot and 16-bit column offsets (10 B per entry against CSR's
  * 12; 32-bit columns where a row spans more than 65,535 columns); it is a
@@ -255,7 +252,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
  * rows per XCD, 1: one wavefront), [12] X rows the 8 parts read, summed,
  * over the pattern's X rows (-1: not computed), [13] the kernel a tiled
  * plan runs: 0 none (untiled), 1 k_rows_ws, 2 k_rows_mfma, 3 k_spmv_chunks,
- * 4 k_rows_cs (lab), 5 (r4) k_panel_chunks (1 < K < 32); [14] chunks of a k_rows_cs plan; [15] (r4) the k_rows_ws
+ * 4 k_rows_cs (lab); [14] chunks of a k_rows_cs plan; [15] (r4) the k_rows_ws
  * geometry (1: one 1024-lane block per CU, 2: two 512-lane blocks, 3: one
  * 768-lane block; 0 other); [16] (r4) 1 if a bind writes the snapshot's real
  * entries from per-quad / per-run descriptors (pads written once at create:

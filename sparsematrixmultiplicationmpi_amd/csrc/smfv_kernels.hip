@@ -358,97 +358,6 @@ __global__ __launch_bounds__(NT) void k_spmv_chunks(const int4 *__restrict__ hdr
 #endif
 
 // ---------------------------------------------------------------------------
-// (r4) k_panel_chunks: the same chunk plan for a narrow panel, 1 < kc < 32
-// columns (SC/...ColumnWise.cpp:34-48: a rank's K/p column window, and any
-// one-device K below the tiled kernel's 32-column panel).  The chunk's
-// entries (values snapshot, 16-bit column offsets) are loaded once; for each
-// group of CG columns every entry gathers its CG X values from the window
-// and its CG products go to LDS (the partial accumulators), then lane t sums
-// row t's products column by column in CSR order (separate multiply and
-// add: bit-identical) and stores CG contiguous doubles of the panel row.
-// One pass over the CSR whatever kc (the untiled row kernel re-streamed it
-// at 1.4 TB/s with 2-lane rows).
-// ---------------------------------------------------------------------------
-template <int NT, int CH, bool WIDE, int CG, bool V2X>
-__global__ __launch_bounds__(NT) void k_panel_chunks(const int4 *__restrict__ hdr, const uint16_t *__restrict__ rs,
-                                                     const uint16_t *__restrict__ off, const int *__restrict__ col,
-                                                     const double *__restrict__ vals,
-                                                     const double *__restrict__ X, int64_t ldx, int kc,
-                                                     double *__restrict__ Y, int64_t ldy)
-{
-    static_assert(CH % (2 * NT) == 0 && CG % 2 == 0, "whole entry pairs per lane, column pairs");
-    constexpr int V2 = CH / (2 * NT);
-    // column-major partial products (column q of entry e at q * CH + e): the
-    // row sums' lanes (one row each, rows ~27 entries apart) then read
-    // spread banks; entry-major made them collide
-    __shared__ double prod[CG * CH];
-    const int c = xcd_remap(blockIdx.x, gridDim.x);
-    const int t = threadIdx.x;
-    const int4 h = hdr[c];  // first row, rows, base column, entries
-    const chunk_d2 *v2 = reinterpret_cast<const chunk_d2 *>(vals + (int64_t)c * CH);
-    const uint32_t *o2 = reinterpret_cast<const uint32_t *>(off + (int64_t)c * CH);
-    const uint64_t *c2 = reinterpret_cast<const uint64_t *>(col + (int64_t)c * CH);
-    chunk_d2 v[V2];
-    int64_t j0[V2], j1[V2];
-#pragma unroll
-    for (int k = 0; k < V2; ++k) {
-        v[k] = __builtin_nontemporal_load(v2 + k * NT + t);
-        if constexpr (WIDE) {
-            const uint64_t cc = __builtin_nontemporal_load(c2 + k * NT + t);
-            j0[k] = (int64_t)(int)(uint32_t)cc;
-            j1[k] = (int64_t)(int)(uint32_t)(cc >> 32);
-        } else {
-            const uint32_t o = __builtin_nontemporal_load(o2 + k * NT + t);
-            j0[k] = (int64_t)(o & 0xFFFFu);
-            j1[k] = (int64_t)(o >> 16);
-        }
-    }
-    const uint16_t *rsc = rs + (int64_t)c * (NT + 1);
-    const int a = rsc[t], b = rsc[t + 1];
-    const double *xb = X + (int64_t)h.z * ldx;
-    for (int c0 = 0; c0 < kc; c0 += CG) {
-#pragma unroll
-        for (int k = 0; k < V2; ++k) {
-            const int e0 = 2 * (k * NT + t);
-            const bool in0 = e0 < h.w, in1 = e0 + 1 < h.w;  // pads and columns past kc gather nothing
-            double x0[CG], x1[CG];
-#pragma unroll
-            for (int q = 0; q < CG; q += 2) {
-                if constexpr (V2X) {  // kc even, X 16-byte aligned with an even stride: pairs of columns
-                    const chunk_d2 z = {0.0, 0.0};
-                    const chunk_d2 p0 = in0 && c0 + q < kc ? *reinterpret_cast<const chunk_d2 *>(xb + j0[k] * ldx + c0 + q) : z;
-                    const chunk_d2 p1 = in1 && c0 + q < kc ? *reinterpret_cast<const chunk_d2 *>(xb + j1[k] * ldx + c0 + q) : z;
-                    x0[q] = p0.x, x0[q + 1] = p0.y, x1[q] = p1.x, x1[q + 1] = p1.y;
-                } else {
-#pragma unroll
-                    for (int h2 = 0; h2 < 2; ++h2) {
-                        x0[q + h2] = in0 && c0 + q + h2 < kc ? xb[j0[k] * ldx + c0 + q + h2] : 0.0;
-                        x1[q + h2] = in1 && c0 + q + h2 < kc ? xb[j1[k] * ldx + c0 + q + h2] : 0.0;
-                    }
-                }
-            }
-#pragma unroll
-            for (int q = 0; q < CG; ++q)
-                reinterpret_cast<chunk_d2 *>(prod + q * CH)[k * NT + t] = chunk_d2{v[k].x * x0[q], v[k].y * x1[q]};
-        }
-        __syncthreads();
-        if (t < h.y) {
-            double acc[CG];
-#pragma unroll
-            for (int q = 0; q < CG; ++q) acc[q] = 0.0;
-            for (int j = a; j < b; ++j)
-#pragma unroll
-                for (int q = 0; q < CG; ++q) acc[q] = acc[q] + prod[q * CH + j];
-            double *y = Y + (int64_t)(h.x + t) * ldy + c0;
-#pragma unroll
-            for (int q = 0; q < CG; ++q)
-                if (c0 + q < kc) y[q] = acc[q];
-        }
-        __syncthreads();  // the products' LDS is rewritten by the next column group
-    }
-}
-
-// ---------------------------------------------------------------------------
 // k_rows_mh: the production row kernel for K even and 16-byte aligned X/Y.
 //
 //  * a block of 256 lanes owns 256/TEAM consecutive rows; it stages its
@@ -2213,10 +2122,11 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
     // K = 1: the chunk plan (k_spmv_chunks) wherever the pattern fits its
     // layout (no row over a chunk, 16-bit column spans); otherwise the plan
     // stays untiled (k_spmv_stream on the live CSR)
-    // (r4) and 1 < K < 32: the same layout, run by k_panel_chunks (a
-    // ColumnWise rank's K/p window, or a narrow K on one device)
-    if (!rc && whole_rows && h_rp && h_ci && m > 0 && K >= 1 && K < TILE_KP &&
-        !(flags & (SMFV_PLAN_NO_TILES | SMFV_PLAN_MFMA | SMFV_PLAN_SIMPLE_ROWS))) {
+    // ((r4) the same layout for 1 < K < 32 -- a ColumnWise rank's K/p window
+    // -- with the products of 4 / 8 / 16 columns in LDS, k_panel_chunks, was
+    // 1.0-7x slower than the untiled row kernel at K/p = 4 / 8 / 16 on cop20k
+    // (profiles/r04/rank_plans) and was removed)
+    if (!rc && whole_rows && h_rp && h_ci && m > 0 && K == 1 && !(flags & (SMFV_PLAN_NO_TILES | SMFV_PLAN_MFMA))) {
         std::vector<int> rpl((size_t)m + 1);
         for (int i = 0; i <= m; ++i) rpl[i] = (int)(h_rp[row_begin + i] - nnz_base);
         SpmvChunkPlan C;
@@ -2548,7 +2458,7 @@ SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS])
     out[10] = plan->mfma ? 1.0 : 0.0;
     out[11] = plan->parts;
     out[12] = plan->footprint;
-    out[13] = !plan->tiled ? 0.0 : plan->cs ? 4.0 : plan->k1 ? (plan->K > 1 ? 5.0 : 3.0) : plan->mfma ? 2.0 : 1.0;
+    out[13] = !plan->tiled ? 0.0 : plan->cs ? 4.0 : plan->k1 ? 3.0 : plan->mfma ? 2.0 : 1.0;
     out[14] = plan->cs_chunks;
     out[15] = plan->tiled && !plan->cs && !plan->k1 && !plan->mfma ? plan->ws_geom : 0;
     out[16] = plan->bind_desc ? 1.0 : 0.0;
@@ -2611,20 +2521,6 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
                       "capturing; synchronize the bind stream before capture");
             return SMFV_ERR_INVALID;
         }
-    }
-    if (plan->k1 && K > 1) {  // (r4) narrow panel
-        if (plan->ntiles > 0) {
-            const bool v2x = K % 2 == 0 && ldx % 2 == 0 && aligned16(d_X);
-#define PK(W_, G_) (v2x ? k_panel_chunks<K1_NT, 1024, W_, G_, true> : k_panel_chunks<K1_NT, 1024, W_, G_, false>)
-            auto kern = plan->k1_wide ? (K <= 4 ? PK(true, 4) : PK(true, 8)) : (K <= 4 ? PK(false, 4) : PK(false, 8));
-#undef PK
-            SMFV_REQUIRE(plan->k1_cap == 1024, "panel chunks need 1,024-entry chunks");
-            hipLaunchKernelGGL(kern, dim3((unsigned)plan->ntiles), dim3(K1_NT), 0, st,
-                               reinterpret_cast<const int4 *>(plan->k1_hdr), plan->k1_rs, plan->k1_off, plan->k1_col,
-                               plan->tvals, d_X, ldx, K, d_Y, ldy);
-            SMFV_LAUNCHED();
-        }
-        return SMFV_OK;
     }
     if (plan->k1) {
         if (plan->ntiles > 0) {

@@ -119,7 +119,7 @@ PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA, PLAN_NATURAL_SEEDS, PLAN_MFMA, PLAN_S
 PLAN_ONE_WAVEFRONT, PLAN_SIMPLE_ROWS, PLAN_CS, PLAN_WS = 64, 128, 256, 512
 PLAN_WS_GEOM1, PLAN_WS_GEOM2, PLAN_WS_GEOM3 = 1024, 2048, 4096
 PLAN_STATS = 17  # SMFV_PLAN_STATS
-PLAN_KERNELS = {0: None, 1: "k_rows_ws", 2: "k_rows_mfma", 3: "k_spmv_chunks", 4: "k_rows_cs", 5: "k_panel_chunks"}
+PLAN_KERNELS = {0: None, 1: "k_rows_ws", 2: "k_rows_mfma", 3: "k_spmv_chunks", 4: "k_rows_cs"}
 
 
 class SpmmPlan:

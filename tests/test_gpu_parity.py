@@ -520,29 +520,32 @@ def _chunk_matrix(seed, m=9000, n=200000):
 
 
 @pytest.mark.parametrize("K", [2, 3, 4, 5, 8, 12, 16, 31])
-def test_panel_chunk_plan_narrow_k(gpu, K):
-    """(r4) 1 < K < 32 takes the chunk layout too (k_panel_chunks: the
-    chunk's entries loaded once, their products for groups of 4 or 8
-    columns in LDS, each row summed in CSR order): bit-identical to the
-    reference's sequential sum for every variant, on the chunk test pattern
-    (empty rows, a wide-column row switching to 32-bit columns), with padded
-    leading dimensions, and as a ColumnWise rank's column window (X + f with
-    the full row stride: SC/...ColumnWise.cpp:34-48)."""
+def test_narrow_k_column_window(gpu, K):
+    """1 < K < 32 (a ColumnWise rank's K/p window, SC/...ColumnWise.cpp:34-48):
+    the untiled row kernel, bit-identical to the reference's sequential sum
+    for every variant but NONZERO (merge path, 1e-12) on the chunk test
+    pattern (empty rows, a row spanning > 2^16 columns), read from a column
+    window of a wider X (X + f, the full row stride) into a padded Y."""
     A = _chunk_matrix(71 + K)
     Kx = 40
     X = np.random.default_rng(72 + K).uniform(-1, 1, (A.numCols, Kx))
     dA = smfv.DeviceCSR(A, gpu)
     dXf = torch.from_numpy(X).to(gpu)
+    absA = np.abs(A.values)
     for f in (0, 7):  # column window [f, f + K) of the 40-wide X
-        Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, np.ascontiguousarray(X[:, f:f + K]))
-        for v in (smfv.Variant.ROWWISE, smfv.Variant.COLUMNWISE, smfv.Variant.NONZERO):
+        Xw = np.ascontiguousarray(X[:, f:f + K])
+        Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, Xw)
+        for v in smfv.Variant:
             plan = smfv.SpmmPlan(v, dA, K)
-            st = plan.stats()
-            assert st["tiled"] and st["kernel"] == "k_panel_chunks", (v, st)
             Yb = torch.full((A.numRows, K + 3), np.nan, dtype=torch.float64, device=gpu)
             plan.run(dXf[:, f:f + K], Yb[:, :K])
             torch.cuda.synchronize()
-            assert np.array_equal(bits(Yb[:, :K].cpu().numpy()), bits(Yref)), (v, f)
+            Y = Yb[:, :K].cpu().numpy()
+            if v == smfv.Variant.NONZERO:
+                scale = oracle.spmm("sequential", A.rowPtr, A.colIndices, absA, np.abs(Xw))
+                assert rel_err(Y, Yref, scale) <= NNZ_TOL, (v, f)
+            else:
+                assert np.array_equal(bits(Y), bits(Yref)), (v, f)
             assert torch.isnan(Yb[:, K:]).all()
 
 
