@@ -993,39 +993,30 @@ __global__ __launch_bounds__(256) void k_gather_vals(int64_t count, const int *_
     }
 }
 
-// (r4) The bind from descriptors: only the real entries of the snapshot are
-// written (its pads were filled once at plan creation, k_fill_f64), and the
-// sources come from a per-PAIR table (4 B per 16-B value pair, instead of a
-// 4-B index per 8-B entry): pt[i] = CSR index of pair i's first value when
-// both are real, -(index + 2) when only the first is, -1 for a pad pair.  A
-// lane binds two pairs (one 8-B table load, four value loads, two stores).
-// Tiles' pairs interleave the 4 rows of a quad, so a wave's value loads are
-// 4 runs of 256 contiguous bytes.
-__global__ __launch_bounds__(256) void k_bind_pairs(int64_t npairs, const int2 *__restrict__ pt,
+// (r4) The bind from "items": an item is up to 4 consecutive non-zeros of
+// one row (tiled plans: entries 4g .. 4g + 3 of a quad's row k) or of one
+// chunk (K = 1 plans).  Item i = {CSR index of its first value, (first value
+// pair << 4) | (stride 4 ? 8 : 0) | real entries}: its values are one
+// contiguous CSR run and land in two value pairs, 4 pairs apart in a tile's
+// quad interleave (stride 4) or adjacent in a chunk.  Items are in snapshot
+// order, so a wave's loads are 32-byte runs of a few rows and its stores
+// fill whole 64-byte groups of pairs; the pads were written once when the
+// plan was created (k_fill_f64).  One item per lane.
+__global__ __launch_bounds__(256) void k_bind_items(int64_t n, const int2 *__restrict__ it,
                                                     const double *__restrict__ va, double *__restrict__ tv)
 {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // pairs 2i, 2i + 1
-    if (2 * i >= npairs) return;
-    const int2 d = 2 * i + 1 < npairs ? pt[i] : int2{reinterpret_cast<const int *>(pt)[2 * i], -1};
-    ws::d2 *o = reinterpret_cast<ws::d2 *>(tv) + 2 * i;
-    const int s0 = d.x >= 0 ? d.x : -d.x - 2, s1 = d.y >= 0 ? d.y : -d.y - 2;
-    double a0 = 0.0, b0 = 0.0, a1 = 0.0, b1 = 0.0;
-    if (d.x != -1) a0 = va[s0];
-    if (d.x >= 0) b0 = va[s0 + 1];
-    if (d.y != -1) a1 = va[s1];
-    if (d.y >= 0) b1 = va[s1 + 1];
-    if (d.x >= 0) o[0] = ws::d2{a0, b0};
-    else if (d.x != -1) reinterpret_cast<double *>(o)[0] = a0;
-    if (d.y >= 0) o[1] = ws::d2{a1, b1};
-    else if (d.y != -1) reinterpret_cast<double *>(o + 1)[0] = a1;
-}
-// contiguous runs (direct rows, K = 1 chunks): {dst entry, src, count}, one block per run
-__global__ __launch_bounds__(256) void k_bind_runs(const int64_t *__restrict__ rd, const double *__restrict__ va,
-                                                   double *__restrict__ tv)
-{
-    const int64_t *d = rd + 3 * (int64_t)blockIdx.x;
-    const int64_t dst = d[0], src = d[1], cnt = d[2];
-    for (int64_t i = threadIdx.x; i < cnt; i += 256) tv[dst + i] = va[src + i];
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int2 d = it[i];
+    const int cnt = d.y & 7;
+    const int64_t p0 = (int64_t)((unsigned)d.y >> 4), p1 = p0 + ((d.y & 8) ? 4 : 1);
+    const double *v = va + d.x;
+    const double a0 = v[0], a1 = cnt > 1 ? v[1] : 0.0, a2 = cnt > 2 ? v[2] : 0.0, a3 = cnt > 3 ? v[3] : 0.0;
+    ws::d2 *o = reinterpret_cast<ws::d2 *>(tv);
+    if (cnt > 1) o[p0] = ws::d2{a0, a1};
+    else reinterpret_cast<double *>(o + p0)[0] = a0;
+    if (cnt > 3) o[p1] = ws::d2{a2, a3};
+    else if (cnt > 2) reinterpret_cast<double *>(o + p1)[0] = a2;
 }
 // (r4) The cut rows of a NONZERO range (at most its first and last row):
 // row i's partial sum over its entries [s[i], e[i]), one block per row.
@@ -1785,10 +1776,9 @@ struct smfv_plan_s {
     int parts = 1;                 // 8: one part of the rows per XCD (build_ws_plan)
     double footprint = -1.0;       // parts_footprint of the 8 parts
     int *tsrc = nullptr;                   // snapshot entry -> CSR index of its value (-1: pad); NULL with descriptors
-    int *bind_pairs = nullptr;             // (r4) bind descriptors: one int per value pair (k_bind_pairs)
-    int64_t *bind_runs = nullptr;          // (r4) 3 int64 per contiguous run (k_bind_runs)
-    int64_t nbind_pairs = 0, nbind_runs = 0;
-    bool bind_desc = false;                // bind from the descriptors (pads filled at creation)
+    int *bind_items = nullptr;             // (r4) 2 ints per bind item (k_bind_items)
+    int64_t nbind_items = 0;
+    bool bind_desc = false;                // bind by k_bind_items (pads filled at creation)
     double *tvals = nullptr;               // the bound values snapshot (tile order, pads -0.0, then direct rows)
     const double *bound_values = nullptr;  // d_values the snapshot came from
     int *ws_grec = nullptr, *ws_lrec = nullptr, *direct_rows = nullptr;
@@ -1822,7 +1812,7 @@ struct smfv_plan_s {
     ~smfv_plan_s()
     {
         delete sub;
-        for (void *q : {(void *)tsrc, (void *)bind_pairs, (void *)bind_runs, (void *)tvals, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
+        for (void *q : {(void *)tsrc, (void *)bind_items, (void *)tvals, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
                         (void *)direct_off, (void *)ws_loff, ws, (void *)mf_rec, (void *)mf_ucols, (void *)mf_bstep,
                         (void *)k1_hdr, (void *)k1_rs, (void *)k1_off, (void *)k1_col, (void *)cs_bs,
                         (void *)cs_trow, (void *)cs_tlast, (void *)cs_crec, (void *)cs_aux})
@@ -1843,40 +1833,49 @@ template <class T> int upload(T **dst, const std::vector<T> &src, size_t &acc)
 
 }  // namespace
 
-// (r4) The snapshot's sources as bind descriptors: a per-pair table for the
-// tiles' pairs [0, npairs) (k_bind_pairs) and contiguous runs for the rest
-// (direct rows, K = 1 chunks; k_bind_runs), checked on the host against the
-// per-entry sources `ts` (each real entry written once, from the same CSR
-// index; pads untouched).  On a match the descriptors are uploaded and the
-// pads written once; otherwise the plan keeps the per-entry gather.
-static int setup_bind(smfv_plan_s *p, const std::vector<int> &ts, const std::vector<int> &pairs,
-                      const std::vector<int64_t> &runs, double pad)
+// (r4) The bind items (k_bind_items) from the snapshot's per-entry sources
+// `ts` (CSR index or -1 for a pad): an item starts at every real entry whose
+// CSR index begins a group of 4 (from its row start for a tiled plan, whose
+// quads interleave rows; from its chunk start for a K = 1 plan, `group_base`
+// gives the group origin of a CSR index), and the items are replayed on the
+// host: they must write every real entry once, from its own source (else the
+// plan keeps the per-entry gather, k_gather_vals).  The pads are written once.
+template <class GroupBase, class Stride4>
+static int setup_bind(smfv_plan_s *p, const std::vector<int> &ts, Stride4 stride4_at, GroupBase group_base, double pad)
 {
     const int64_t n = (int64_t)ts.size();
-    std::vector<int> chk((size_t)n, -1);
-    bool ok = 2 * (int64_t)pairs.size() <= n;
-    for (size_t i = 0; ok && i < pairs.size(); ++i) {
-        const int d = pairs[i];
-        if (d == -1) continue;
-        const int64_t src = d >= 0 ? d : -(int64_t)d - 2;
-        ok = src >= 0 && chk[2 * i] == -1;
-        if (ok) chk[2 * i] = (int)src;
-        if (ok && d >= 0) chk[2 * i + 1] = (int)(src + 1);
+    std::vector<int> items;
+    bool ok = n / 2 < ((int64_t)1 << 27);
+    for (int64_t e = 0; ok && e < n; ++e) {
+        const int j = ts[(size_t)e];
+        if (j < 0 || (j - group_base(j)) % 4 != 0) continue;
+        ok = e % 2 == 0;  // a group starts a value pair
+        const bool stride4 = stride4_at(e);
+        // the group's real entries: consecutive sources at the layout's positions
+        int cnt = 1;
+        auto pos = [&](int h) { return 2 * (e / 2 + (h >= 2 ? (stride4 ? 4 : 1) : 0)) + (h & 1); };
+        while (ok && cnt < 4 && pos(cnt) < n && ts[(size_t)pos(cnt)] == j + cnt && group_base(j + cnt) == group_base(j))
+            ++cnt;
+        items.push_back(j);
+        items.push_back((int)(((e / 2) << 4) | (stride4 ? 8 : 0) | cnt));
     }
-    for (size_t r = 0; ok && r < runs.size() / 3; ++r)
-        for (int64_t i = 0; ok && i < runs[3 * r + 2]; ++i) {
-            const int64_t e = runs[3 * r] + i;
+    // replay: every real entry written once, from its own source
+    std::vector<int> chk((size_t)n, -1);
+    for (size_t i = 0; ok && i < items.size(); i += 2) {
+        const int j = items[i], d = items[i + 1], cnt = d & 7;
+        const int64_t p0 = (unsigned)d >> 4, p1 = p0 + ((d & 8) ? 4 : 1);
+        for (int h = 0; h < cnt && ok; ++h) {
+            const int64_t e = 2 * (h < 2 ? p0 : p1) + (h & 1);
             ok = e < n && chk[(size_t)e] == -1;
-            if (ok) chk[(size_t)e] = (int)(runs[3 * r + 1] + i);
+            if (ok) chk[(size_t)e] = j + h;
         }
+    }
     ok = ok && chk == ts;
     int rc = SMFV_OK;
     if (ok) {
         p->bind_desc = true;
-        p->nbind_pairs = (int64_t)pairs.size();
-        p->nbind_runs = (int64_t)runs.size() / 3;
-        rc = upload(&p->bind_pairs, pairs, p->dev_bytes);
-        if (!rc) rc = upload(&p->bind_runs, runs, p->dev_bytes);
+        p->nbind_items = (int64_t)items.size() / 2;
+        rc = upload(&p->bind_items, items, p->dev_bytes);
     } else {
         rc = upload(&p->tsrc, ts, p->dev_bytes);
     }
@@ -2093,28 +2092,26 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                     std::vector<int64_t> doff;
                     doff.reserve(W.direct.size());
                     for (int r : W.direct) {
+                        if (ts.size() % 2) ts.push_back(-1);  // (r4) each direct row starts a value pair (bind items)
                         doff.push_back((int64_t)ts.size());
                         for (int j = rpl[r]; j < rpl[r + 1]; ++j) ts.push_back((int)(nnz_base + j));
                     }
                     p->snapshot = (int64_t)ts.size();
-                    // bind descriptors: the tiles' value pairs (from the per-entry
-                    // sources: a pair is two consecutive entries of one row), the direct rows
-                    std::vector<int> pt((size_t)(W.ventries / 2));
-                    for (size_t i = 0; i < pt.size(); ++i) {
-                        const int a = ts[2 * i], b = ts[2 * i + 1];
-                        pt[i] = a < 0 ? -1 : b == a + 1 ? a : -a - 2;
-                    }
-                    std::vector<int64_t> runs;
-                    for (size_t i = 0; i < W.direct.size(); ++i) {
-                        const int r = W.direct[i];
-                        runs.insert(runs.end(), {doff[i], nnz_base + rpl[r], (int64_t)(rpl[r + 1] - rpl[r])});
-                    }
                     if (!rc) rc = upload(&p->ws_grec, W.grec, p->dev_bytes);
                     if (!rc) rc = upload(&p->ws_lrec, W.lrec, p->dev_bytes);
                     if (!rc) rc = upload(&p->ws_loff, W.loff, p->dev_bytes);
                     if (!rc) rc = upload(&p->direct_rows, W.direct, p->dev_bytes);
                     if (!rc) rc = upload(&p->direct_off, doff, p->dev_bytes);
-                    if (!rc) rc = setup_bind(p, ts, pt, runs, -0.0);
+                    // bind items: groups of 4 from each row's start (global CSR index -> its row's start)
+                    std::vector<int> rowstart;
+                    rowstart.reserve((size_t)p->nnz);
+                    for (int r = 0; r < m; ++r)
+                        for (int j = rpl[r]; j < rpl[r + 1]; ++j) rowstart.push_back((int)nnz_base + rpl[r]);
+                    const int64_t tiles_end = W.ventries;  // tile pairs interleave 4 rows; direct rows are contiguous
+                    if (!rc)
+                        rc = setup_bind(
+                            p, ts, [&](int64_t e) { return e < tiles_end; },
+                            [&](int j) { return rowstart[(size_t)(j - nnz_base)]; }, -0.0);
                 }
             }
         }
@@ -2141,16 +2138,19 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
             for (int &q : C.tsrc)
                 if (q >= 0) q += (int)nnz_base;
             p->snapshot = (int64_t)C.tsrc.size();
-            // bind descriptors: each chunk's entries are one contiguous CSR run
-            std::vector<int64_t> runs;
-            for (int c = 0; c < C.nchunks; ++c) {
-                const int64_t cnt = C.hdr[(size_t)c * 4 + 3], dst = (int64_t)c * C.cap;
-                if (cnt > 0) runs.insert(runs.end(), {dst, (int64_t)C.tsrc[(size_t)dst], cnt});
-            }
             if (!rc) rc = upload(&p->k1_hdr, C.hdr, p->dev_bytes);
             if (!rc) rc = upload(&p->k1_rs, C.rs, p->dev_bytes);
             if (!rc) rc = C.wide ? upload(&p->k1_col, C.col, p->dev_bytes) : upload(&p->k1_off, C.off, p->dev_bytes);
-            if (!rc) rc = setup_bind(p, C.tsrc, {}, runs, -0.0);
+            // bind items: groups of 4 from each chunk's start
+            std::vector<int> chunkstart((size_t)p->nnz, 0);
+            for (int c = 0; c < C.nchunks; ++c) {
+                const int64_t cnt = C.hdr[(size_t)c * 4 + 3], s0 = C.tsrc[(size_t)c * C.cap];
+                for (int64_t i = 0; i < cnt; ++i) chunkstart[(size_t)(s0 + i - nnz_base)] = (int)s0;
+            }
+            if (!rc)
+                rc = setup_bind(
+                    p, C.tsrc, [](int64_t) { return false; }, [&](int j) { return chunkstart[(size_t)(j - nnz_base)]; },
+                    -0.0);
         }
     }
     // (r4) NONZERO over a range that cuts rows (SC/...NonZeroElement.cpp:24-67
@@ -2392,17 +2392,11 @@ SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, voi
     hipStream_t st = as_stream(stream);
     const int64_t cnt = plan->snapshot;
     if (plan->bind_desc) {
-        // (r4) real entries only, from the descriptors (pads were written at creation)
-        if (plan->nbind_pairs > 0) {
-            const int64_t lanes = (plan->nbind_pairs + 1) / 2;
-            hipLaunchKernelGGL(k_bind_pairs, dim3((unsigned)((lanes + 255) / 256)), dim3(256), 0, st,
-                               plan->nbind_pairs, reinterpret_cast<const int2 *>(plan->bind_pairs), d_values,
+        // (r4) the real entries from the bind items (pads written at creation)
+        if (plan->nbind_items > 0) {
+            hipLaunchKernelGGL(k_bind_items, dim3((unsigned)((plan->nbind_items + 255) / 256)), dim3(256), 0, st,
+                               plan->nbind_items, reinterpret_cast<const int2 *>(plan->bind_items), d_values,
                                plan->tvals);
-            SMFV_LAUNCHED();
-        }
-        if (plan->nbind_runs > 0) {
-            hipLaunchKernelGGL(k_bind_runs, dim3((unsigned)plan->nbind_runs), dim3(256), 0, st, plan->bind_runs,
-                               d_values, plan->tvals);
             SMFV_LAUNCHED();
         }
     } else if (cnt > 0) {
