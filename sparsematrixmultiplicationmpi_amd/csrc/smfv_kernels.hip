@@ -1011,12 +1011,21 @@ __global__ __launch_bounds__(256) void k_bind_items(int64_t n, const int2 *__res
     const int cnt = d.y & 7;
     const int64_t p0 = (int64_t)((unsigned)d.y >> 4), p1 = p0 + ((d.y & 8) ? 4 : 1);
     const double *v = va + d.x;
-    const double a0 = v[0], a1 = cnt > 1 ? v[1] : 0.0, a2 = cnt > 2 ? v[2] : 0.0, a3 = cnt > 3 ? v[3] : 0.0;
     ws::d2 *o = reinterpret_cast<ws::d2 *>(tv);
+    if (cnt == 4) {
+        // two 16-byte loads (8-byte aligned: the global unaligned mode takes
+        // them) instead of four 8-byte ones: half the load instructions
+        ws::d2 lo, hi;
+        __builtin_memcpy(&lo, v, 16);
+        __builtin_memcpy(&hi, v + 2, 16);
+        o[p0] = lo;
+        o[p1] = hi;
+        return;
+    }
+    const double a0 = v[0], a1 = cnt > 1 ? v[1] : 0.0, a2 = cnt > 2 ? v[2] : 0.0;
     if (cnt > 1) o[p0] = ws::d2{a0, a1};
     else reinterpret_cast<double *>(o + p0)[0] = a0;
-    if (cnt > 3) o[p1] = ws::d2{a2, a3};
-    else if (cnt > 2) reinterpret_cast<double *>(o + p1)[0] = a2;
+    if (cnt > 2) reinterpret_cast<double *>(o + p1)[0] = a2;
 }
 // (r4) The cut rows of a NONZERO range (at most its first and last row):
 // row i's partial sum over its entries [s[i], e[i]), one block per row.
