@@ -209,10 +209,10 @@ def cpu_baseline(A, K: int, variant: str, sample: str | None = None, budget_s: f
                 sweep[str(c)] = round(flops / t / 1e9, 4)
         nproc_point = None
         if sweep_ranks and tag != "S" and nproc not in counts:
-            t = _ref_run(A, K, tag, nproc, ref, 3, 90.0)
+            t = _ref_run(A, K, tag, nproc, ref, 3, 30.0)
             nproc_point = {"ranks": nproc, "GFLOPs": round(flops / t / 1e9, 4) if t else None,
                            "note": "mpiexec -n nproc (SURVEY 8d); nproc counts the whole host, this process's "
-                                   "share is 16 CPUs, so it oversubscribes; None = over its 90 s cap or failed"}
+                                   "share is 16 CPUs, so it oversubscribes; None = over its 30 s cap or failed"}
         top = str(counts[-1])
         if top in sweep:
             o0 = (_ref_run(A, K, tag, counts[-1], ref0, 3, budget_s * 6)

@@ -18,7 +18,7 @@ for cfg in ${CFGS:-cop20k_k32}; do
     cut -c 1-300 "$OUT/bench_$cfg.json"
   fi
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$cfg" -o prof --output-format csv \
-      -- python3 "$ROOT/bench.py" --config $cfg --no-cpu-baseline --no-vendor --no-warm --steps 200 --warmup 20 \
+      -- python3 "$ROOT/bench.py" --config $cfg --no-cpu-baseline --no-vendor --no-warm --no-rebind --steps 200 --warmup 20 \
       > "$OUT/prof_$cfg.json" 2> "$OUT/prof_$cfg.log")
   rc=$?; echo "rocprof $cfg rc=$rc"; [ $rc -eq 0 ] || exit $rc
   find "$OUT/prof_$cfg" -name "*kernel_stats.csv" -exec head -n 8 {} \; | cut -c 1-200
