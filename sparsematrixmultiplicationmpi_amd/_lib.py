@@ -157,6 +157,8 @@ def _load() -> ctypes.CDLL:
             "(make -C sparsematrixmultiplicationmpi_amd/csrc). There is no CPU fallback.")
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in (dict(_SIGS, **_LAB_SIGS) if LAB else _SIGS).items():
+        if name in _LAB_SIGS and not hasattr(lib, name):
+            continue  # a product build staged as the lab library (A/B runs)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

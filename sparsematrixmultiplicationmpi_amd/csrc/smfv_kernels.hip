@@ -777,7 +777,13 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
                 b1 = *reinterpret_cast<const d2 *>(lds + r3);
             };
             constexpr unsigned LO = 0x010c000cu, HI = 0x030c020cu;  // rows 0, 1 / rows 2, 3 of the word
+            // offsets two batches ahead: ln (batch b), lnn (b + 1, read during
+            // batch b - 1), ln2 (b + 2, read in batch b after its second-half X
+            // reads) -- so the X reads of batch b + 1 wait only for an offsets
+            // read a whole batch old, and the reads behind it stay in flight
+            // (a counted lgkmcnt, no drain)
             u2 ln = Lq[0];
+            u2 lnn = Lq[4 * min(1, max(blast, 0))];
             d2 vn[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) vn[q] = Vq[4 * q];
@@ -785,15 +791,12 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
             rdx(ln.x, LO, xa0[0], xa1[0], xa0[1], xa1[1]);
             rdx(ln.x, HI, xa0[2], xa1[2], xa0[3], xa1[3]);
             for (int b = 0; b < nbat; ++b) {
+                const int bn = min(b + 1, blast);
                 rdx(ln.y, LO, xc0[0], xc1[0], xc0[1], xc1[1]);  // second half of batch b
                 rdx(ln.y, HI, xc0[2], xc1[2], xc0[3], xc1[3]);
                 __builtin_amdgcn_sched_barrier(0);
-                // next batch's offsets (the last batch re-reads itself); volatile
-                // keeps the read here, behind this batch's X reads
-                const int bn = min(b + 1, blast);
-                ln = *(const volatile __attribute__((address_space(3))) u2 *)(Lq + 4 * bn);
-                // the first half's FP64 goes after it: it covers the offsets'
-                // latency before the next batch's X addresses need them
+                // offsets of batch b + 2 (the last batch re-reads itself)
+                const u2 ln2 = *(const volatile __attribute__((address_space(3))) u2 *)(Lq + 4 * min(b + 2, blast));
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -806,8 +809,8 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
 #pragma unroll
                 for (int q = 0; q < 2; ++q)
                     vn[q] = *(const volatile __attribute__((address_space(3))) d2 *)(Vq + 4 * (4 * bn + q));
-                rdx(ln.x, LO, xa0[0], xa1[0], xa0[1], xa1[1]);  // first half of batch b + 1
-                rdx(ln.x, HI, xa0[2], xa1[2], xa0[3], xa1[3]);
+                rdx(lnn.x, LO, xa0[0], xa1[0], xa0[1], xa1[1]);  // first half of batch b + 1
+                rdx(lnn.x, HI, xa0[2], xa1[2], xa0[3], xa1[3]);
                 __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the second half's FP64
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -818,6 +821,8 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
 #pragma unroll
                 for (int q = 2; q < 4; ++q)
                     vn[q] = *(const volatile __attribute__((address_space(3))) d2 *)(Vq + 4 * (4 * bn + q));
+                ln = lnn;
+                lnn = ln2;
             }
             // xa / vn / ln hold the first half of batch blast: its first rem
             // entries end the row (a wave runs a step if any of its teams needs it)
