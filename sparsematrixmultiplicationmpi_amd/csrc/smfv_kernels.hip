@@ -362,7 +362,7 @@ __global__ __launch_bounds__(NT) void k_spmv_chunks(const int4 *__restrict__ hdr
 //
 //  * a block of 256 lanes owns 256/TEAM consecutive rows; it stages its
 //    row_ptr slice and its non-zero range (col, val) into LDS with one
-//    coalesced pass (chunks of STAGE_CAP non-zeros if it holds more), so the
+//    coalesced pass (chunks of stage_cap(TEAM) non-zeros if it holds more), so the
 //    dependent global round trips are row_ptr -> CSR -> X only;
 //  * a team of TEAM lanes owns one row; lane t holds H double2 column groups
 //    at columns 2t + 2*TEAM*h (h < H), i.e. each of the H 16-byte loads of a
@@ -377,7 +377,12 @@ __global__ __launch_bounds__(NT) void k_spmv_chunks(const int4 *__restrict__ hdr
 //    in CSR order (separate multiply and add: bit-identical to the
 //    reference's sequential loop).
 // ---------------------------------------------------------------------------
-constexpr int STAGE_CAP = 1024;  // non-zeros staged per block pass (12 KiB)
+// non-zeros staged per block pass: sized so a block's rows (256 / TEAM of
+// them) usually fit one pass at ~22 non-zeros per row -- with a 1,024 cap a
+// 128-row block (TEAM 2, a 4-column rank panel) ran three passes with a
+// third of its teams live in each; 36 KiB at TEAM 2 still leaves 4 blocks
+// (16 waves) per CU
+constexpr int stage_cap(int team) { return team <= 1 ? 4096 : team == 2 ? 3072 : team == 4 ? 1536 : 1024; }
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <int TEAM, int H, int U, bool BUF>
@@ -391,6 +396,7 @@ __global__ __launch_bounds__(256) void k_rows_mh(int row_begin, int nrows,
 {
     constexpr int RPB = 256 / TEAM;
     constexpr int CP = 2 * TEAM * H;  // columns per pass
+    constexpr int STAGE_CAP = stage_cap(TEAM);
     constexpr int PER_THREAD = STAGE_CAP / 256;
     __shared__ int s_rp[RPB + 1];
     __shared__ int s_ci[STAGE_CAP];
