@@ -615,7 +615,7 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
         const int nb = gridDim.x >> 3;  // blocks per XCD
         const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
         const int first = xr.first[x], end = xr.first[x + 1];
-        if (chunked) {
+        if (chunked & 1) {
             const int S = end - first, q = S / nb, r = S % nb;
             t0 = first + j * q + min(j, r);
             cnt = q + (j < r ? 1 : 0);
@@ -630,6 +630,11 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
     }
     const int tlast = t0 + (cnt - 1) * tstep;
     const int nunits = cnt * npanel;
+    // (r4) a narrow column window (chunked bits 16-23: K = 4, 8 or 16, one
+    // panel): the loaders stage only the window's bytes of each union row and
+    // the teams store only its columns (the other columns of the image are
+    // never written, their sums never stored)
+    const int kwin = (chunked >> 16) & 0xFF;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const unsigned lds0 = (unsigned)(uintptr_t)lds;  // LDS byte address of the block's image
     if (wv >= CW) {
@@ -697,7 +702,7 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
             for (int i = 0; i < PPW; ++i) {
                 const int piece = wl + LW * i;  // 1 KiB = union rows 4*piece .. +3 (pieces dealt round-robin)
                 const int u = 4 * piece + (lane >> 4);
-                if (4 * piece < nu && u < UCAP) {
+                if (4 * piece < nu && u < UCAP && (kwin == 0 || 2 * (lane & 15) < kwin)) {
                     if constexpr (SADDR)
                         dma16s<false>(X + cp, xo[i], xb + piece * 1024);
                     else
@@ -855,8 +860,12 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
             // DMAs: stores deferred into the next unit, among the loaders'
             // DMA issue, measured 25.6 -> 28.1 us)
             double *y = Y + (int64_t)row * ldy + p * TILE_KP + 2 * tl;
-            __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y + 16 * par));
-            __builtin_nontemporal_store(acc1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
+            if (kwin == 0) {
+                __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y + 16 * par));
+                __builtin_nontemporal_store(acc1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
+            } else if (2 * tl < kwin) {  // columns 2 tl, 2 tl + 1 of the window: acc0 on even teams, acc1 on odd
+                __builtin_nontemporal_store(par ? acc1 : acc0, reinterpret_cast<d2 *>(y));
+            }
         }
         if (++p == npanel) p = 0, ++it;
         barrier_lds();  // X slot (u & 1) is free for unit u + 2, meta slot for tile it + 1
@@ -890,7 +899,7 @@ static auto pick_ws(int geom, bool fma, bool saddr)
 // row, X gathered straight from HBM, CSR order (bit-identical).  `rows` are
 // block-local (Y row), row_begin + row indexes the CSR; the values come from
 // the plan's bound snapshot (tv + doff[team], CSR order), like the tiles'.
-__global__ __launch_bounds__(256) void k_rows_list(int nrows, const int *__restrict__ rows,
+__global__ __launch_bounds__(256) void k_rows_list(int nrows, int kwin, const int *__restrict__ rows,
                                                    const int64_t *__restrict__ doff, int row_begin,
                                                    const int *__restrict__ rp, const int *__restrict__ ci,
                                                    const double *__restrict__ tv,
@@ -905,6 +914,13 @@ __global__ __launch_bounds__(256) void k_rows_list(int nrows, const int *__restr
     const int j0 = rp[row_begin + row];
     const double *vrow = tv + doff[team] - j0;
     double2 acc0 = make_double2(0.0, 0.0), acc1 = make_double2(0.0, 0.0);
+    if (kwin) {  // (r4) a narrow window (K = 4, 8, 16): columns 2 tl, 2 tl + 1 only
+        if (2 * tl >= kwin) return;
+        for (int jj = j0; jj < rp[row_begin + row + 1]; ++jj)
+            acc0 = VecT<2>::madd(acc0, vrow[jj], *reinterpret_cast<const double2 *>(X + (int64_t)ci[jj] * ldx + 2 * tl));
+        *reinterpret_cast<double2 *>(Y + (int64_t)row * ldy + 2 * tl) = acc0;
+        return;
+    }
     for (int jj = j0; jj < rp[row_begin + row + 1]; ++jj) {
         const double *px = X + (int64_t)ci[jj] * ldx + cp + 2 * tl;
         const double v = vrow[jj];
@@ -1964,7 +1980,10 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
     // nnz-balanced merge path
     const bool whole_rows = variant != SMFV_NONZERO ||
                             (h_rp && h_rp[row_begin] == nnz_base && h_rp[row_begin + m] == nnz_end);
-    if (!rc && whole_rows && h_rp && h_ci && m > 0 && p->nnz > 0 && K > 0 && K % TILE_KP == 0 &&
+    // (r4) K = 4 / 8 / 16 (a ColumnWise rank's panel): the same tiles, one
+    // narrow column window (k_rows_ws stages and stores only its columns)
+    const bool tile_k = K % TILE_KP == 0 || K == 4 || K == 8 || K == 16;
+    if (!rc && whole_rows && h_rp && h_ci && m > 0 && p->nnz > 0 && K > 0 && tile_k &&
         !(flags & SMFV_PLAN_NO_TILES)) {  // (no non-zeros: nothing to stage)
         std::vector<int> rpl((size_t)m + 1);
         for (int i = 0; i <= m; ++i) rpl[i] = (int)(h_rp[row_begin + i] - nnz_base);
@@ -1982,7 +2001,7 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
             go = p->est_reuse >= SMFV_TILE_MIN_REUSE;
         }
         if (go) plan_parts(caps, flags, m, n, rpl.data(), cil, &p->footprint);
-        if (go && (flags & SMFV_PLAN_MFMA)) {
+        if (go && (flags & SMFV_PLAN_MFMA) && K % TILE_KP == 0) {
             MfmaPlan F;
             std::string err;
             if (!build_mfma_plan(m, n, rpl.data(), cil, F, &err, caps)) {
@@ -2022,7 +2041,8 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
         // (lab only since r4)
         // column-streamed tiles (k_rows_cs) where asked for; a pattern the
         // layout does not take (unsorted rows, ...) keeps k_rows_ws
-        if (!rc && go && !(flags & SMFV_PLAN_MFMA) && (flags & SMFV_PLAN_CS) && !(flags & SMFV_PLAN_WS)) {
+        if (!rc && go && !(flags & SMFV_PLAN_MFMA) && (flags & SMFV_PLAN_CS) && !(flags & SMFV_PLAN_WS) &&
+            K % TILE_KP == 0) {
             CsPlan C;
             std::string err;
             if (build_cs_plan(m, n, rpl.data(), cil, C, &err, caps)) {
@@ -2630,8 +2650,14 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         WsXcd xr;
         for (int x = 0; x <= 8; ++x) xr.first[x] = plan->ws_xcd[x];
         const int threads = ws_geom(plan->ws_geom).threads();
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3((unsigned)threads), 0, st, xr, K / TILE_KP, chunked,
-                           plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
+        // (r4) K = 4 / 8 / 16: one panel, a narrow column window (chunked bits 16-23)
+        const bool narrow = K < TILE_KP;
+#ifdef SMFV_LAB
+        if (narrow) kern = pick_ws(plan->ws_geom, plan->fma, saddr);  // the lab copies know no window
+#endif
+        if (narrow) chunked = (chunked & 1) | (K << 16);
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3((unsigned)threads), 0, st, xr,
+                           narrow ? 1 : K / TILE_KP, chunked, plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();
 #ifdef SMFV_LAB
         if (abl == 8)
@@ -2647,8 +2673,8 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
 #endif
     }
     if (plan->ndirect > 0) {
-        hipLaunchKernelGGL(k_rows_list, dim3((unsigned)((plan->ndirect + 31) / 32), (unsigned)(K / TILE_KP)),
-                           dim3(256), 0, st, plan->ndirect, plan->direct_rows, plan->direct_off, plan->row_begin,
+        hipLaunchKernelGGL(k_rows_list, dim3((unsigned)((plan->ndirect + 31) / 32), (unsigned)std::max(1, K / TILE_KP)),
+                           dim3(256), 0, st, plan->ndirect, K < TILE_KP ? K : 0, plan->direct_rows, plan->direct_off, plan->row_begin,
                            d_row_ptr, d_col_idx, plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();
     }

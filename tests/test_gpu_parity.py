@@ -359,6 +359,35 @@ def test_tiled_plan_bitwise(gpu, K):
                     assert plan.stats()["tiled"]
 
 
+@pytest.mark.parametrize("K", [4, 8, 16])
+def test_tiled_narrow_window_bitwise(gpu, K):
+    """(r4) K = 4 / 8 / 16 -- a ColumnWise rank's K/p panel (SC/...ColumnWise.cpp:34-48)
+    -- on the tiled kernel: the column window [f, f + K) of a 32-wide X (X + f,
+    the full row stride) into a Y panel whose padded stride must stay
+    untouched (NaN): the kernel stages and stores only the window's columns.
+    Bit-identical to the reference's sequential sum, including direct rows
+    (rows wider than the LDS union, k_rows_list)."""
+    rng = np.random.default_rng(100 + K)
+    for A in (smfv.gen_fem27(5000, 12, 12, 0.83, K),
+              smfv.gen_random_rows(6000, 5000, 16, 2.0, 1500, K)):  # rows up to 1500 wide
+        X = rng.uniform(-1, 1, (A.numCols, 32))
+        dA = smfv.DeviceCSR(A, gpu)
+        dXf = torch.from_numpy(X).to(gpu)
+        for f in (0, 32 - K):
+            Xw = np.ascontiguousarray(X[:, f:f + K])
+            Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, Xw)
+            for mode in ("force", "auto"):
+                for v in (smfv.Variant.SEQUENTIAL, smfv.Variant.ROWWISE, smfv.Variant.COLUMNWISE):
+                    plan = smfv.SpmmPlan(v, dA, K, tiles=mode)
+                    Yb = torch.full((A.numRows, K + 2), np.nan, dtype=torch.float64, device=gpu)
+                    plan.run(dXf[:, f:f + K], Yb[:, :K])
+                    torch.cuda.synchronize()
+                    assert np.array_equal(bits(Yb[:, :K].cpu().numpy()), bits(Yref)), (f, mode, v, plan.stats())
+                    assert torch.isnan(Yb[:, K:]).all()
+                    if mode == "force":
+                        assert plan.stats()["tiled"]
+
+
 def test_tiled_plan_stats_cop20k(gpu):
     A = smfv.cop20k_surrogate()
     plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(A, gpu), 32)
