@@ -110,7 +110,9 @@ SMFV_API int smfv_spmm_csr_f64(int variant, int m, int n, int64_t nnz,
 
 /* ---- plans: analysed once per (matrix pattern, K), executed many times --
  * The plan owns all device workspace (merge-path carries for NONZERO) and,
- * with K a multiple of 32, a clustered
+ * with K a multiple of 32 (or K = 4, 8, 16: one narrow column window, e.g. a
+ * ColumnWise rank's K/p panel; the kernel stages and stores only the window's
+ * columns, X and Y 16-byte aligned with even strides), a clustered
  * row-tile analysis of the pattern (h_col_idx needed): tiles of <= 64 rows
  * grown by adjacency whose distinct X rows (<= 239) fit a 60 KiB LDS image,
  * with a tile-ordered copy of the values and 16-bit X-row offsets.  The tiled
