@@ -125,8 +125,9 @@ PLAN_KERNELS = {0: None, 1: "k_rows_ws", 2: "k_rows_mfma", 3: "k_spmv_chunks", 4
 class SpmmPlan:
     """One variant of Y = A*X analysed once for (A, K) (smfv_plan_create):
     device workspace allocated up front and, for K % 32 == 0 or K = 4 / 8 /
-    16 (one narrow column window), the row-tile analysis that lets the kernel stage re-used X rows in LDS.  run() is a
-    pure asynchronous launch sequence (capturable into a hipGraph).
+    16 (one narrow column window), the row-tile analysis that lets the kernel
+    stage re-used X rows in LDS.  run() is a pure asynchronous launch
+    sequence (capturable into a hipGraph).
 
     tiles: "auto" (stage when re-use >= 3), "off", or "force".  fma: opt-in
     fused multiply-add in the tiled kernel (SMFV_PLAN_FMA).  rows=(begin,
