@@ -204,7 +204,8 @@ def cpu_baseline(A, K: int, variant: str, sample: str | None = None, budget_s: f
         counts = [1] if tag == "S" else ([1, 2, 4, 8, 16] if sweep_ranks else [16])
         sweep = {}
         for c in counts:
-            t = _ref_run(A, K, tag, c, ref, 5 if c == counts[-1] and sweep_ranks else 3, budget_s * 6)
+            # the reported point (the top rank count): median of 10 calls
+            t = _ref_run(A, K, tag, c, ref, 10 if c == counts[-1] and sweep_ranks else 3, budget_s * 6)
             if t:
                 sweep[str(c)] = round(flops / t / 1e9, 4)
         nproc_point = None
@@ -222,7 +223,7 @@ def cpu_baseline(A, K: int, variant: str, sample: str | None = None, budget_s: f
                     "binding": "MPICH hydra " + " ".join(MPI_BIND) + " (one rank per core), -launcher fork",
                     "nproc_point": nproc_point,
                     "sample": f"{what}, reference {name} (SC sources, g++ -O3) under MPICH mpiexec -n {top}, "
-                              f"median of {5 if sweep_ranks else 3} calls incl. gather + FatVector rebuild"
+                              f"median of {10 if sweep_ranks else 3} calls incl. gather + FatVector rebuild"
                               f"{'; 1/2/4/8/16-rank sweep and the -O0 build beside it' if sweep_ranks else ''}; "
                               f"wall {time.time() - t0:.1f}s",
                     "seconds_per_call": flops / (sweep[top] * 1e9),
