@@ -592,7 +592,7 @@ template <int CW, int LW, int PPW, int UCAP, int NCAP> struct Lay {
 struct WsXcd {
     int first[9];  // XCD x runs tiles [first[x], first[x + 1]) of the plan's order
 };
-template <int CW, int LW, int PPW, int UCAP, int NCAP, bool FMA = false, bool SADDR = true>
+template <int CW, int LW, int PPW, int UCAP, int NCAP, bool FMA = false, bool SADDR = true, bool NARROW = false>
 __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsXcd xr, int npanel, int chunked,
                                                      const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
@@ -630,11 +630,15 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
     }
     const int tlast = t0 + (cnt - 1) * tstep;
     const int nunits = cnt * npanel;
-    // (r4) a narrow column window (chunked bits 16-23: K = 4, 8 or 16, one
-    // panel): the loaders stage only the window's bytes of each union row and
-    // the teams store only its columns (the other columns of the image are
-    // never written, their sums never stored)
-    const int kwin = (chunked >> 16) & 0xFF;
+    // (r4) NARROW: a narrow column window (chunked bits 16-23: K = 4, 8 or
+    // 16, one panel).  The loaders stage the window's bytes of each union row
+    // into BOTH 128-byte halves of its image row (lanes 8-15 of a row repeat
+    // lanes 0-7: the same cache lines, one DMA), so every team reads its
+    // columns from its own half as at K = 32 (conflict-free) and needs one
+    // accumulator: half the X reads and FP64 of a full panel; the teams store
+    // only the window's columns
+    const int kwin = NARROW ? (chunked >> 16) & 0xFF : 0;
+    constexpr int XLANE = NARROW ? 7 : 15;  // a loader lane's 16-byte column chunk: lane & XLANE
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const unsigned lds0 = (unsigned)(uintptr_t)lds;  // LDS byte address of the block's image
     if (wv >= CW) {
@@ -676,7 +680,7 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
             if constexpr (SADDR)
                 if (p == 0)  // per tile: the union rows' byte offsets (panels add to the scalar base)
 #pragma unroll
-                    for (int i = 0; i < PPW; ++i) xo[i] = (unsigned)uc[i] * ldxb + 16u * (unsigned)(lane & 15);
+                    for (int i = 0; i < PPW; ++i) xo[i] = (unsigned)uc[i] * ldxb + 16u * (unsigned)(lane & XLANE);
             auto stage_meta = [&]() {
                 const unsigned mb = lds0 + SL_M + ms * MSLOT;
                 if constexpr (SADDR) {
@@ -702,11 +706,11 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
             for (int i = 0; i < PPW; ++i) {
                 const int piece = wl + LW * i;  // 1 KiB = union rows 4*piece .. +3 (pieces dealt round-robin)
                 const int u = 4 * piece + (lane >> 4);
-                if (4 * piece < nu && u < UCAP && (kwin == 0 || 2 * (lane & 15) < kwin)) {
+                if (4 * piece < nu && u < UCAP && (!NARROW || 2 * (lane & 7) < kwin)) {
                     if constexpr (SADDR)
                         dma16s<false>(X + cp, xo[i], xb + piece * 1024);
                     else
-                        dma16<false>(X + (int64_t)uc[i] * ldx + cp + 2 * (lane & 15), xb + piece * 1024);
+                        dma16<false>(X + (int64_t)uc[i] * ldx + cp + 2 * (lane & XLANE), xb + piece * 1024);
                 }
             }
             if (p == 0) stage_meta();
@@ -784,8 +788,10 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
                     : "=v"(r3) : "v"(xo1), "v"(pw));
                 a0 = *reinterpret_cast<const d2 *>(lds + r0);
                 b0 = *reinterpret_cast<const d2 *>(lds + r1);
-                a1 = *reinterpret_cast<const d2 *>(lds + r2);
-                b1 = *reinterpret_cast<const d2 *>(lds + r3);
+                if constexpr (!NARROW) {
+                    a1 = *reinterpret_cast<const d2 *>(lds + r2);
+                    b1 = *reinterpret_cast<const d2 *>(lds + r3);
+                }
             };
             constexpr unsigned LO = 0x010c000cu, HI = 0x030c020cu;  // rows 0, 1 / rows 2, 3 of the word
             // offsets two batches ahead: ln (batch b), lnn (b + 1, read during
@@ -812,7 +818,7 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     acc0 = madd(acc0, (k & 1) ? vn[k >> 1].y : vn[k >> 1].x, xa0[k]);
-                    acc1 = madd(acc1, (k & 1) ? vn[k >> 1].y : vn[k >> 1].x, xa1[k]);
+                    if constexpr (!NARROW) acc1 = madd(acc1, (k & 1) ? vn[k >> 1].y : vn[k >> 1].x, xa1[k]);
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 // each value pair is re-read in place once its FP64 has issued
@@ -826,7 +832,7 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     acc0 = madd(acc0, (k & 1) ? vn[2 + (k >> 1)].y : vn[2 + (k >> 1)].x, xc0[k]);
-                    acc1 = madd(acc1, (k & 1) ? vn[2 + (k >> 1)].y : vn[2 + (k >> 1)].x, xc1[k]);
+                    if constexpr (!NARROW) acc1 = madd(acc1, (k & 1) ? vn[2 + (k >> 1)].y : vn[2 + (k >> 1)].x, xc1[k]);
                 }
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -839,20 +845,20 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
             // entries end the row (a wave runs a step if any of its teams needs it)
             if (rem >= 2) {
                 acc0 = madd(acc0, vn[0].x, xa0[0]);
-                acc1 = madd(acc1, vn[0].x, xa1[0]);
+                if constexpr (!NARROW) acc1 = madd(acc1, vn[0].x, xa1[0]);
                 acc0 = madd(acc0, vn[0].y, xa0[1]);
-                acc1 = madd(acc1, vn[0].y, xa1[1]);
+                if constexpr (!NARROW) acc1 = madd(acc1, vn[0].y, xa1[1]);
                 if (rem >= 4) {
                     acc0 = madd(acc0, vn[1].x, xa0[2]);
-                    acc1 = madd(acc1, vn[1].x, xa1[2]);
+                    if constexpr (!NARROW) acc1 = madd(acc1, vn[1].x, xa1[2]);
                     acc0 = madd(acc0, vn[1].y, xa0[3]);
-                    acc1 = madd(acc1, vn[1].y, xa1[3]);
+                    if constexpr (!NARROW) acc1 = madd(acc1, vn[1].y, xa1[3]);
                     if (rem >= 6) {
                         rdx(ln.y, LO, xc0[0], xc1[0], xc0[1], xc1[1]);
                         acc0 = madd(acc0, vn[2].x, xc0[0]);
-                        acc1 = madd(acc1, vn[2].x, xc1[0]);
+                        if constexpr (!NARROW) acc1 = madd(acc1, vn[2].x, xc1[0]);
                         acc0 = madd(acc0, vn[2].y, xc0[1]);
-                        acc1 = madd(acc1, vn[2].y, xc1[1]);
+                        if constexpr (!NARROW) acc1 = madd(acc1, vn[2].y, xc1[1]);
                     }
                 }
             }
@@ -860,11 +866,12 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
             // DMAs: stores deferred into the next unit, among the loaders'
             // DMA issue, measured 25.6 -> 28.1 us)
             double *y = Y + (int64_t)row * ldy + p * TILE_KP + 2 * tl;
-            if (kwin == 0) {
+            if constexpr (NARROW) {
+                if (2 * tl < kwin)  // columns 2 tl, 2 tl + 1 of the window (from either image half)
+                    __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y));
+            } else {
                 __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y + 16 * par));
                 __builtin_nontemporal_store(acc1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
-            } else if (2 * tl < kwin) {  // columns 2 tl, 2 tl + 1 of the window: acc0 on even teams, acc1 on odd
-                __builtin_nontemporal_store(par ? acc1 : acc0, reinterpret_cast<d2 *>(y));
             }
         }
         if (++p == npanel) p = 0, ++it;
@@ -877,18 +884,27 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
 #endif
 
 // the product instances of k_rows_ws: geometry (smfv_plan.h WsGeom) x FMA x SADDR
-#define SMFV_WS_INST(G_) k_rows_ws<G_.cw, G_.lw, G_.ppw, G_.ucap, G_.ncap, FMA, SADDR>
-template <bool FMA, bool SADDR> constexpr auto WS1 = SMFV_WS_INST(WS_GEOM1);
-template <bool FMA, bool SADDR> constexpr auto WS2 = SMFV_WS_INST(WS_GEOM2);
-template <bool FMA, bool SADDR> constexpr auto WS3 = SMFV_WS_INST(WS_GEOM3);
+#define SMFV_WS_INST(G_) k_rows_ws<G_.cw, G_.lw, G_.ppw, G_.ucap, G_.ncap, FMA, SADDR, NARROW>
+template <bool FMA, bool SADDR, bool NARROW = false> constexpr auto WS1 = SMFV_WS_INST(WS_GEOM1);
+template <bool FMA, bool SADDR, bool NARROW = false> constexpr auto WS2 = SMFV_WS_INST(WS_GEOM2);
+template <bool FMA, bool SADDR, bool NARROW = false> constexpr auto WS3 = SMFV_WS_INST(WS_GEOM3);
 #undef SMFV_WS_INST
-static auto pick_ws(int geom, bool fma, bool saddr)
+template <bool NARROW>
+static auto pick_ws_n(int geom, bool fma, bool saddr)
 {
     if (geom == 2)
-        return fma ? (saddr ? WS2<true, true> : WS2<true, false>) : (saddr ? WS2<false, true> : WS2<false, false>);
+        return fma ? (saddr ? WS2<true, true, NARROW> : WS2<true, false, NARROW>)
+                   : (saddr ? WS2<false, true, NARROW> : WS2<false, false, NARROW>);
     if (geom == 3)
-        return fma ? (saddr ? WS3<true, true> : WS3<true, false>) : (saddr ? WS3<false, true> : WS3<false, false>);
-    return fma ? (saddr ? WS1<true, true> : WS1<true, false>) : (saddr ? WS1<false, true> : WS1<false, false>);
+        return fma ? (saddr ? WS3<true, true, NARROW> : WS3<true, false, NARROW>)
+                   : (saddr ? WS3<false, true, NARROW> : WS3<false, false, NARROW>);
+    return fma ? (saddr ? WS1<true, true, NARROW> : WS1<true, false, NARROW>)
+               : (saddr ? WS1<false, true, NARROW> : WS1<false, false, NARROW>);
+}
+// (r4) narrow: a K = 4 / 8 / 16 window (one accumulator per lane)
+static auto pick_ws(int geom, bool fma, bool saddr, bool narrow = false)
+{
+    return narrow ? pick_ws_n<true>(geom, fma, saddr) : pick_ws_n<false>(geom, fma, saddr);
 }
 
 #ifdef SMFV_LAB
@@ -2652,10 +2668,10 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         const int threads = ws_geom(plan->ws_geom).threads();
         // (r4) K = 4 / 8 / 16: one panel, a narrow column window (chunked bits 16-23)
         const bool narrow = K < TILE_KP;
-#ifdef SMFV_LAB
-        if (narrow) kern = pick_ws(plan->ws_geom, plan->fma, saddr);  // the lab copies know no window
-#endif
-        if (narrow) chunked = (chunked & 1) | (K << 16);
+        if (narrow) {
+            kern = pick_ws(plan->ws_geom, plan->fma, saddr, true);
+            chunked = (chunked & 1) | (K << 16);
+        }
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3((unsigned)threads), 0, st, xr,
                            narrow ? 1 : K / TILE_KP, chunked, plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();
