@@ -883,7 +883,7 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
 #include "lab/ws_lab.inc"  // the instrumented lab copy (libsmfv_lab.so only)
 #endif
 
-// the product instances of k_rows_ws: geometry (smfv_plan.h WsGeom) x FMA x SADDR
+// the product instances of k_rows_ws: geometry (smfv_plan.h WsGeom) x FMA x SADDR x NARROW
 #define SMFV_WS_INST(G_) k_rows_ws<G_.cw, G_.lw, G_.ppw, G_.ucap, G_.ncap, FMA, SADDR, NARROW>
 template <bool FMA, bool SADDR, bool NARROW = false> constexpr auto WS1 = SMFV_WS_INST(WS_GEOM1);
 template <bool FMA, bool SADDR, bool NARROW = false> constexpr auto WS2 = SMFV_WS_INST(WS_GEOM2);
