@@ -388,6 +388,34 @@ def test_tiled_narrow_window_bitwise(gpu, K):
                         assert plan.stats()["tiled"]
 
 
+@pytest.mark.parametrize("tk", ["ws1", "ws2", "ws3", "fma"])
+def test_tiled_narrow_window_instances(gpu, tk):
+    """(r4) Every NARROW instance of k_rows_ws (geometries 1 / 2 / 3, and the
+    FMA opt-in within 1e-12 x sum|a||x|) on an 8-column window of a 32-wide
+    X, on a pattern large enough for several units per block."""
+    K, f = 8, 16
+    A = smfv.gen_fem27(40000, 30, 30, 0.83, 5)
+    X = np.random.default_rng(5).uniform(-1, 1, (A.numCols, 32))
+    Xw = np.ascontiguousarray(X[:, f:f + K])
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, Xw)
+    dA = smfv.DeviceCSR(A, gpu)
+    dXf = torch.from_numpy(X).to(gpu)
+    plan = (smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles="force", fma=True) if tk == "fma"
+            else smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles="force", tiled_kernel=tk))
+    st = plan.stats()
+    assert st["tiled"] and (tk == "fma" or st["ws_geom"] == int(tk[-1])), st
+    Yb = torch.full((A.numRows, K + 2), np.nan, dtype=torch.float64, device=gpu)
+    plan.run(dXf[:, f:f + K], Yb[:, :K])
+    torch.cuda.synchronize()
+    Y = Yb[:, :K].cpu().numpy()
+    if tk == "fma":
+        scale = oracle.spmm("sequential", A.rowPtr, A.colIndices, np.abs(A.values), np.abs(Xw))
+        assert np.all(np.abs(Y - Yref) <= 1e-12 * scale + 1e-300)
+    else:
+        assert np.array_equal(bits(Y), bits(Yref)), st
+    assert torch.isnan(Yb[:, K:]).all()
+
+
 def test_tiled_plan_stats_cop20k(gpu):
     A = smfv.cop20k_surrogate()
     plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(A, gpu), 32)
