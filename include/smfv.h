@@ -257,8 +257,8 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
  * 4 k_rows_cs (lab); [14] chunks of a k_rows_cs plan; [15] (r4) the k_rows_ws
  * geometry (1: one 1024-lane block per CU, 2: two 512-lane blocks, 3: one
  * 768-lane block; 0 other); [16] (r4) 1 if a bind writes the snapshot's real
- * entries from per-quad / per-run descriptors (pads written once at create:
- * k_bind_quads, k_bind_runs), 0 if it gathers every entry by index */
+ * entries from bind items of up to 4 consecutive non-zeros (pads written once
+ * at create: k_bind_items), 0 if it gathers every entry by index */
 #define SMFV_PLAN_STATS 17
 SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS]);
 SMFV_API int smfv_plan_destroy(smfv_plan_t plan);
