@@ -11,7 +11,11 @@ rotates over enough copies of (A, X, Y) that every launch streams from HBM
 rather than from the 256 MiB Infinity Cache (cold); the same-copy (warm)
 rate is reported beside it.
 
-N > 1 (one process per GPU, launched by torch.distributed.run): ONE problem
+N > 1 (one process per GPU).  Under torch.distributed.run (WORLD_SIZE set)
+every process is one rank and --gpus must equal WORLD_SIZE; a plain
+`python bench.py --gpus N` starts the N ranks itself, as children
+(torch.distributed.run on 127.0.0.1, no exec), and re-prints rank 0's line --
+the reference's `mpirun -np P ./prog` (SC/scripts/mpi.sub:97).  ONE problem
 decomposed over the ranks as the reference's RowWise does
 (SC/...RowWise.cpp:26-29): each rank runs its row block (a tiled plan where
 the pattern re-uses X rows), then one RCCL all-gather of the Y blocks over
@@ -520,6 +524,8 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
     if world > 1:
         dist.init_process_group("gloo")
     comm = D.Communicator.from_torch_distributed()
+    rccl_n = comm.nranks()  # the ranks RCCL itself counts (ncclCommCount), reported as n_gpus
+    ndevs = _devices_used(dev, world)
     dl.enter("inputs + plan")
     dA = smfv.DeviceCSR(A, dev)
     X = torch.empty((n, K), dtype=torch.float64, device=dev)
@@ -577,8 +583,9 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
         out = {
             "metric": metric_for("syn80m_k32", K, "ROWWISE"),
             "value": round(flops / (ms_step * 1e-3) / 1e9, 3), "unit": "GFLOP/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+            "n_gpus": rccl_n, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
             "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "ranks": {"rccl_nranks": rccl_n, "processes": world, "distinct_devices": ndevs},
             "data": f"synthetic: {m}x{m}, 16 uniform-random columns/row (splitmix64 seed 42), X hash 1..100 (seed 43)",
             "config": {"workload": f"syn80m_k32: {m}x{m} x K={K}, ROWWISE row-partitioned over {world} GPU(s)"
                                    " + RCCL all-gather of Y", "m": m, "n": n, "nnz": nnz_tot, "K": K,
@@ -655,6 +662,8 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
         if comm is not None:
             comm.close()
         return err or "the RCCL communicator failed on another rank"
+    rccl_n = comm.nranks()  # the ranks RCCL itself counts (ncclCommCount), reported as n_gpus
+    ndevs = _devices_used(dev, world)
     dl.enter("inputs + distributed plans")
     X_host = inputs.generateLargeFatVector(n, K)
     prob_bytes = algorithmic_bytes(m, n, nnz, K)
@@ -729,8 +738,9 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
         out = {
             "metric": metric_for(args.config, K, variant),
             "value": round(flops / (ms_step * 1e-3) / 1e9, 3),
-            "unit": "GFLOP/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "unit": "GFLOP/s", "n_gpus": rccl_n, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms_step, 6), "higher_is_better": True, "scaling": "strong",
+            "ranks": {"rccl_nranks": rccl_n, "processes": world, "distinct_devices": ndevs},
             "vs_baseline": None, "dtype": "f64",
             "data": f"synthetic: {label}; X = rand()%100+1 (glibc seed 1)",
             "config": {"workload": f"{args.config}: {label} x K={K}, {variant} decomposed over {world} GPUs "
@@ -892,9 +902,103 @@ def _x_rows_touched_nnz(A, s: int, e: int) -> int:
     return int(np.unique(np.asarray(A.colIndices[s:e])).size) if e > s else 0
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` (N > 1) without WORLD_SIZE: start the N ranks as
+    fresh child processes -- torch.distributed.run on 127.0.0.1, one rank per
+    GPU, this same script and arguments -- before anything touches the GPU
+    (no exec: the parent only waits), then re-print rank 0's JSON line as
+    this process's one stdout line.  Everything else the ranks write goes to
+    stderr.  The exit status is the ranks' (torch.distributed.run's).  The
+    line's n_gpus is what the ranks measured (the RCCL communicator's own
+    count in decomposed mode), and a line whose n_gpus is not N makes the
+    exit status non-zero."""
+    import signal
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + argv
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    print(f"[bench] --gpus {n} without WORLD_SIZE: starting {n} ranks: {' '.join(cmd[1:])}", file=sys.stderr,
+          flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+
+    def forward(sig, _frame):  # a timeout / kill of the parent ends the ranks too
+        proc.send_signal(sig)
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, forward)
+    lines = []
+    for line in proc.stdout:
+        if line.lstrip().startswith("{"):
+            lines.append(line.strip())
+        sys.stderr.write(line)
+        sys.stderr.flush()
+    rc = proc.wait()
+    out = None
+    for line in reversed(lines):
+        try:
+            obj = json.loads(line)
+        except ValueError:
+            continue
+        if "metric" in obj or "dry_run" in obj:
+            out = obj
+            break
+    if out is None:
+        print(json.dumps({"metric": HEADLINE_METRIC, "value": None, "unit": "GFLOP/s", "n_gpus": n,
+                          "error": f"the {n} ranks printed no result line (exit status {rc})"}), flush=True)
+        return rc or 5
+    out["launcher"] = {"ranks_started": n, "how": "bench.py --gpus N without WORLD_SIZE: N child ranks via "
+                                                  "torch.distributed.run --nproc-per-node N (127.0.0.1)"}
+    print(json.dumps(out), flush=True)
+    if rc == 0 and out.get("n_gpus") != n:
+        print(f"[bench] the ranks reported n_gpus {out.get('n_gpus')}, not {n}", file=sys.stderr)
+        return 6
+    return rc
+
+
+def dry_run(world: int, rank: int, local: int) -> None:
+    """--dry-run: the ranks start and meet (gloo), nothing touches the GPU;
+    rank 0 prints who came (tests the launcher on a CPU host)."""
+    import torch.distributed as dist
+    me = {"rank": rank, "local_rank": local, "pid": os.getpid()}
+    ranks = [me]
+    if world > 1:
+        dist.init_process_group("gloo")
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+        seen = dist.get_world_size()
+        dist.destroy_process_group()
+    else:
+        seen = 1
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": seen, "ranks": ranks}), flush=True)
+
+
+def _devices_used(dev, world: int) -> int:
+    """Distinct GPUs (PCI domain:bus:device) the ranks run on, over gloo."""
+    import torch
+    import torch.distributed as dist
+    pr = torch.cuda.get_device_properties(dev)
+    key = f"{getattr(pr, 'pci_domain_id', 0)}:{getattr(pr, 'pci_bus_id', dev.index)}:" \
+          f"{getattr(pr, 'pci_device_id', 0)}"
+    if world == 1:
+        return 1
+    keys = [None] * world
+    dist.all_gather_object(keys, key)
+    return len(set(keys))
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); > 1 without WORLD_SIZE starts them itself (torch.distributed.run); "
+                         "under torch.distributed.run it must equal WORLD_SIZE")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="start the ranks and have them meet (gloo) without touching the GPU; rank 0 prints them")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="cop20k_k32", choices=sorted(CONFIGS))
@@ -943,9 +1047,20 @@ def main() -> None:
                          "before a diagnostic JSON line and exit status 4 (0 = no watchdog)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        print(json.dumps({"metric": HEADLINE_METRIC, "value": None, "unit": "GFLOP/s", "n_gpus": world,
+                          "error": f"--gpus {args.gpus} but WORLD_SIZE={world}: the launcher started a different "
+                                   "number of ranks than asked"}), flush=True)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        dry_run(world, rank, local)
+        return
     kind, K, variant = CONFIGS[args.config]
     variant = args.variant or variant
     if kind == "syn80m":
@@ -991,6 +1106,8 @@ def main() -> None:
         # rank runs its own copy of the problem (a decomposed-mode fallback
         # arrives with the group already up)
         dist.init_process_group("gloo")
+    procs = dist.get_world_size() if world > 1 else 1  # the ranks that actually joined
+    ndevs = _devices_used(dev, world)
 
     # ---- resident problem copies ----------------------------------------
     X_host = inputs.generateLargeFatVector(n, K) if cop else None
@@ -1137,7 +1254,9 @@ def main() -> None:
             "metric": metric_for(args.config, K, variant),
             "value": round(value, 3),
             "unit": "GFLOP/s",
-            "n_gpus": world,
+            "n_gpus": procs,
+            "ranks": {"processes": procs, "distinct_devices": ndevs,
+                      "note": "replicas: one independent problem per rank, no RCCL"},
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 6),

@@ -336,6 +336,10 @@ SMFV_API int smfv_comm_init(smfv_comm_t *comm, int nranks, int rank,
 SMFV_API int smfv_comm_destroy(smfv_comm_t comm);
 SMFV_API int smfv_comm_rank(smfv_comm_t comm);
 SMFV_API int smfv_comm_size(smfv_comm_t comm);
+/* The number of ranks the RCCL communicator itself reports (ncclCommCount),
+ * i.e. how many processes actually joined it -- not the size the caller
+ * asked for.  (the reference's MPI_Comm_size(MPI_COMM_WORLD), SC/main.cpp:16) */
+SMFV_API int smfv_comm_count(smfv_comm_t comm, int *nranks);
 /* In-place broadcast of `bytes` device bytes from root's d_buf to every
  * rank's d_buf (ncclBroadcast over xGMI): the device-resident form of the
  * reference's input distribution (SC/main.cpp:106-143, 9x MPI_Bcast).

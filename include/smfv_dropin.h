@@ -30,6 +30,11 @@
 // (r4) It also grows the caller's heap once (SMFV_HEAP_PREFAULT_MB, default
 // 96; 0 = off): freed heap stays mapped and that much is faulted in, so the
 // first result FatVectors do not pay a page fault per 4 KiB.
+// (r5) PROCESS-WIDE SIDE EFFECT: with the prefault on, this sets the
+// caller's glibc allocator to M_MMAP_THRESHOLD = 32 MiB (allocations below
+// it come from the heap, not fresh mmaps) and M_TRIM_THRESHOLD = prefault +
+// 32 MiB (free heap up to that size stays mapped), for the rest of the
+// process.  Set SMFV_HEAP_PREFAULT_MB=0 to leave the allocator untouched.
 // Returns its wall time (seconds).  Optional: the first call does
 // it otherwise, inside its own time.
 double smfvInitDevice();

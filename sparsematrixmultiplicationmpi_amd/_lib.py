@@ -84,6 +84,7 @@ _SIGS = {
     "smfv_comm_destroy": (c_int, [c_void_p]),
     "smfv_comm_rank": (c_int, [c_void_p]),
     "smfv_comm_size": (c_int, [c_void_p]),
+    "smfv_comm_count": (c_int, [c_void_p, _PI]),
     "smfv_comm_bcast": (c_int, [c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     "smfv_dist_workspace_bytes": (c_int, [c_void_p, c_int, c_int, c_int64, _PI, c_int,
                                           POINTER(c_size_t)]),

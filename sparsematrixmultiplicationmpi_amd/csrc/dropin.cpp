@@ -852,14 +852,33 @@ DROPIN_API FatVector sparseMatrixFatVectorMultiplyNonZeroElement(const SparseMat
 // (M_TRIM_THRESHOLD), serve the outer arrays from the heap rather than fresh
 // mmaps (M_MMAP_THRESHOLD), and touch SMFV_HEAP_PREFAULT_MB (default 96) of
 // heap in the arenas the rebuild threads will use, then free it: the first
-// results then land in faulted pages.  0 disables it.
+// results then land in faulted pages.  0 disables it (and leaves the
+// caller's allocator settings alone).
+//
+// (r5) glibc versions that check it cap M_MMAP_THRESHOLD at
+// HEAP_MAX_SIZE / 2 = 32 MiB on 64-bit and reject larger values; r4 asked for
+// 64 MiB without checking the result (this image's glibc 2.35 accepts it --
+// checked with a probe -- but a refusal would have left the threshold pinned
+// at 128 KiB by the M_TRIM_THRESHOLD call that follows, since setting either
+// switches off glibc's dynamic threshold).  32 MiB is accepted everywhere and
+// covers the outer array of any FatVector up to 1.4 M rows (24 B per row
+// vector).  The trim
+// threshold is the prefault size plus a margin, not 1 GiB: this is a
+// process-wide change to the caller's allocator (documented in
+// smfv_dropin.h), so it is kept to what the prefault needs.  Both return
+// values are checked; a refusal is reported on stderr and the prefault
+// skipped.
 static void prefault_heap()
 {
     const char *e = std::getenv("SMFV_HEAP_PREFAULT_MB");
     const long mb = e ? std::atol(e) : 96;
     if (mb <= 0) return;
-    mallopt(M_MMAP_THRESHOLD, 64 << 20);
-    mallopt(M_TRIM_THRESHOLD, 1 << 30);
+    const int mmap_thr = 32 << 20;
+    const long trim_thr = std::min<long>((mb + 32) << 20, 0x7fffffffL);
+    if (mallopt(M_MMAP_THRESHOLD, mmap_thr) != 1 || mallopt(M_TRIM_THRESHOLD, (int)trim_thr) != 1) {
+        std::fprintf(stderr, "smfvInitDevice: mallopt refused the heap settings; heap prefault skipped\n");
+        return;
+    }
     const int nt = (int)std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency()));  // par_rows' threads
     const size_t per = ((size_t)mb << 20) / (size_t)(nt + 1);
     auto touch = [per]() {

@@ -117,6 +117,13 @@ SMFV_API int smfv_comm_destroy(smfv_comm_t comm)
 SMFV_API int smfv_comm_rank(smfv_comm_t comm) { return comm ? comm->rank : -1; }
 SMFV_API int smfv_comm_size(smfv_comm_t comm) { return comm ? comm->nranks : -1; }
 
+SMFV_API int smfv_comm_count(smfv_comm_t comm, int *nranks)
+{
+    SMFV_REQUIRE(comm && nranks, "null argument");
+    SMFV_NCCL(ncclCommCount(comm->nccl, nranks));
+    return SMFV_OK;
+}
+
 SMFV_API int smfv_comm_bcast(smfv_comm_t comm, void *d_buf, size_t bytes, int root, void *stream)
 {
     SMFV_REQUIRE(comm && (d_buf || bytes == 0) && root >= 0 && root < comm->nranks, "bad argument");

@@ -74,6 +74,12 @@ class Communicator:
     def handle(self) -> c_void_p:
         return self._handle
 
+    def nranks(self) -> int:
+        """The ranks RCCL itself counts in this communicator (ncclCommCount)."""
+        n = c_int(0)
+        call("smfv_comm_count", self._handle, byref(n))
+        return n.value
+
     def close(self) -> None:
         if self._handle:
             call("smfv_comm_destroy", self._handle)

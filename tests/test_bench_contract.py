@@ -60,3 +60,41 @@ def test_phase_deadline_prints_a_line_and_exits_4():
             "d = bench.Deadline(0.3, 0, 1, 'm'); d.enter('x'); d.cancel(); time.sleep(1); print('done')") % ROOT
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and r.stdout.strip() == "done"
+
+
+def _env_without_world():
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["PYTHONPATH"] = ROOT
+    return env
+
+
+def test_gpus_n_starts_n_ranks_itself():
+    """(r5) `python bench.py --gpus 2` with no WORLD_SIZE starts
+    two ranks as children (torch.distributed.run) instead of timing one GPU;
+    --dry-run has them meet over gloo without touching a GPU.  stdout is ONE
+    JSON line (rank 0's, re-printed by the parent)."""
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=240, env=_env_without_world(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(out) == 1, r.stdout
+    line = json.loads(out[0])
+    assert line["dry_run"] and line["n_gpus"] == 2
+    assert sorted(x["rank"] for x in line["ranks"]) == [0, 1]
+    assert len({x["pid"] for x in line["ranks"]}) == 2 and os.getpid() not in {x["pid"] for x in line["ranks"]}
+    assert line["launcher"]["ranks_started"] == 2
+
+
+def test_gpus_must_match_world_size():
+    """Under a launcher, --gpus N with a different WORLD_SIZE is refused with
+    one JSON line and a non-zero status (never a silent 1-GPU line)."""
+    import subprocess
+    env = _env_without_world()
+    env["WORLD_SIZE"] = "3"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode == 2
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["value"] is None and "WORLD_SIZE=3" in line["error"]
