@@ -668,73 +668,109 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     X_host = inputs.generateLargeFatVector(n, K)
     prob_bytes = algorithmic_bytes(m, n, nnz, K)
     ncopies = max(1, min(16, math.ceil(args.cold_bytes / prob_bytes) + 1))
+    V = smfv.Variant[variant]
+    rows = V in (smfv.Variant.ROWWISE, smfv.Variant.SEQUENTIAL)
+    # the plans timed per copy: the value's step first (the default plan:
+    # work-balanced row blocks, all-gather to every rank), then beside it the
+    # reference's exchange semantics (blocks to rank 0 only, MPI_Gatherv /
+    # MPI_Reduce, SC/...RowWise.cpp:85-87), the reference's equal-row
+    # partition (SC/...RowWise.cpp:26-29) and the chunked exchange
+    # (SMFV_DIST_CHUNKS: chunk j's all-gatherv overlapped with chunk j + 1's
+    # compute)
+    kinds = {"value": dict(to_all=True, partition=args.partition)}
+    kinds["gather_to_root"] = dict(to_all=False, partition=args.partition)
+    if rows:
+        kinds["reference_rows"] = dict(to_all=True, partition="reference" if args.partition == "balanced"
+                                       else "balanced")
+        if args.chunks > 1:
+            kinds[f"chunked{args.chunks}"] = dict(to_all=True, partition=args.partition, chunks=args.chunks)
     copies, t_plan = [], 0.0
     for c in range(ncopies):
         dA = smfv.DeviceCSR(A, dev)
         dX = torch.from_numpy(X_host).to(dev)
         dY = torch.zeros((m, K), dtype=torch.float64, device=dev)
         t0 = time.time()
-        P = D.DistPlan(comm, smfv.Variant[variant], dA, K, to_all=True, tiles=args.tiles)
-        # the same share with the reference's exchange semantics: gather to
-        # rank 0 only (MPI_Gatherv / MPI_Reduce to the root)
-        Pr = D.DistPlan(comm, smfv.Variant[variant], dA, K, to_all=False, tiles=args.tiles)
+        plans = {k: D.DistPlan(comm, V, dA, K, tiles=args.tiles, **kw) for k, kw in kinds.items()}
         torch.cuda.synchronize()
         t_plan += time.time() - t0
-        copies.append((P, dX, dY, Pr))
+        copies.append((plans, dX, dY))
     # at least one untimed step per copy before any capture: RCCL sets up its
     # peer connections on a communicator's first collective, which a graph
     # capture must not contain
     dl.enter("warm-up (first collectives: RCCL connection set-up)")
     for i in range(max(args.warmup, ncopies)):
-        P, dX, dY, Pr = copies[i % ncopies]
-        P.run(dX, dY)
-        Pr.run(dX, dY)
+        plans, dX, dY = copies[i % ncopies]
+        for P in plans.values():
+            P.run(dX, dY)
     torch.cuda.synchronize()
     dl.enter("timed steps")
-    ms_step, how = _graph_or_eager(lambda i: copies[i % ncopies][0].run(copies[i % ncopies][1],
-                                                                         copies[i % ncopies][2]), args.steps, world)
-    ms_loc, how_loc = _graph_or_eager(lambda i: copies[i % ncopies][0].run_local(copies[i % ncopies][1],
-                                                                                copies[i % ncopies][2]),
-                                      args.steps, world)
-    ms_root, _ = _graph_or_eager(lambda i: copies[i % ncopies][3].run(copies[i % ncopies][1], copies[i % ncopies][2]),
-                                 args.steps, world)
+
+    def timed_plan(key, local=False):
+        def step(i):
+            plans, dX, dY = copies[i % ncopies]
+            (plans[key].run_local if local else plans[key].run)(dX, dY)
+        return _graph_or_eager(step, args.steps, world)
+    ms_step, how = timed_plan("value")
+    ms_loc, how_loc = timed_plan("value", local=True)
+    beside = {}
+    for key in kinds:
+        if key == "value":
+            continue
+        ms_k, how_k = timed_plan(key)
+        ms_kl, _ = timed_plan(key, local=True)
+        beside[key] = (ms_k, ms_kl, how_k)
     # correctness after timing: every rank's Y is the whole product (TO_ALL),
     # against the untiled row kernel (pinned to the reference by the tests;
-    # not the tiled kernel the ranks' shares run)
+    # not the tiled kernel the ranks' shares run) -- the value's plan and,
+    # for ROWWISE, the other TO_ALL plans
     dl.enter("result check")
-    P, dX, dY, _ = copies[0]
-    dY.fill_(float("nan"))
-    P.run(dX, dY)
-    torch.cuda.synchronize()
-    ref_plan = smfv.SpmmPlan(smfv.Variant.SEQUENTIAL, P.A, K, tiles="off")
+    plans, dX, dY = copies[0]
+    ref_plan = smfv.SpmmPlan(smfv.Variant.SEQUENTIAL, plans["value"].A, K, tiles="off")
     Yseq = torch.empty_like(dY)
     ref_plan.run(dX, Yseq)
-    mabs, _ = smfv.compare(Yseq, dY)
-    ok = mabs == 0.0 if variant != "NONZERO" else mabs <= 1e-6
+    ok = True
+    for key, kw in kinds.items():
+        if not kw["to_all"]:
+            continue
+        dY.fill_(float("nan"))
+        plans[key].run(dX, dY)
+        torch.cuda.synchronize()
+        mabs, _ = smfv.compare(Yseq, dY)
+        ok &= (mabs == 0.0) if variant != "NONZERO" else (mabs <= 1e-6)
     # secondary: independent copies (every rank its own whole problem)
-    reps = [(smfv.SpmmPlan(smfv.Variant[variant], Pc.A, K, tiles=args.tiles), dXc, dYc) for Pc, dXc, dYc, _ in copies]
+    reps = [(smfv.SpmmPlan(V, pl["value"].A, K, tiles=args.tiles), dXc, dYc) for pl, dXc, dYc in copies]
     torch.cuda.synchronize()
     ms_rep, _ = _graph_or_eager(lambda i: reps[i % ncopies][0].run(reps[i % ncopies][1], reps[i % ncopies][2]),
                                 args.steps, world)
-    first, last, _, _ = D.exchange_plan(smfv.Variant[variant], m, nnz, A.rowPtr, K, world)
-    if variant == "ROWWISE":
+    first, last, _, _ = plans["value"].partition()
+    if rows:
         r0, r1 = int(first[rank]), int(last[rank]) + 1
         loc_bytes = 12 * (int(A.rowPtr[r1]) - int(A.rowPtr[r0])) + 4 * (r1 - r0 + 1) + \
             8 * _x_rows_touched(A, r0, r1) * K + 8 * (r1 - r0) * K
     else:
         loc_bytes = prob_bytes // world
-    t = torch.tensor([ms_step, ms_loc, ms_rep, float(loc_bytes) / max(ms_loc, 1e-9), 0.0 if ok else 1.0, ms_root],
-                     dtype=torch.float64)
+    keys = list(beside)
+    vals = [ms_step, ms_loc, ms_rep, float(loc_bytes) / max(ms_loc, 1e-9), 0.0 if ok else 1.0]
+    for key in keys:
+        vals += [beside[key][0], beside[key][1]]
+    t = torch.tensor(vals, dtype=torch.float64)
     tmin = t.clone()
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(tmin, op=dist.ReduceOp.MIN)
     dl.cancel()
-    ms_step, ms_loc, ms_rep, _, bad, ms_root = t.tolist()
+    tl = t.tolist()
+    ms_step, ms_loc, ms_rep, _, bad = tl[:5]
     flops = 2.0 * nnz * K
-    st = P.stats()
+    st = plans["value"].stats()
     if rank == 0:
         loc_gbps = float(tmin[3]) * 1e-6  # the slowest rank's local bytes / its local time (GB/s)
+        others = {}
+        for i, key in enumerate(keys):
+            ms_k, ms_kl = tl[5 + 2 * i], tl[6 + 2 * i]
+            others[key] = {"ms_per_step": round(ms_k, 6), "rank_local_ms": round(ms_kl, 6),
+                           "exchange_ms": round(ms_k - ms_kl, 6), "plan": kinds[key],
+                           "GFLOPs": round(flops / (ms_k * 1e-3) / 1e9, 3), "timing": beside[key][2]}
         out = {
             "metric": metric_for(args.config, K, variant),
             "value": round(flops / (ms_step * 1e-3) / 1e9, 3),
@@ -746,7 +782,8 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
             "config": {"workload": f"{args.config}: {label} x K={K}, {variant} decomposed over {world} GPUs "
                                    "(rank-local plan + RCCL all-gather of Y)",
                        "m": m, "n": n, "nnz": nnz, "K": K, "variant": variant,
-                       "parallelism": f"{variant} partition over {world} ranks (SC partition formulas), "
+                       "parallelism": f"{variant} partition over {world} ranks "
+                                      f"({'work-balanced row blocks' if rows and args.partition == 'balanced' else 'SC partition formulas'}), "
                                       "A and X replicated, Y all-gathered", "copies_rotated": ncopies},
             "roofline": {"bound": "hbm", "achieved": round(loc_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(loc_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
@@ -756,22 +793,26 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
                          "timing": f"rank-local kernel alone ({how_loc}), slowest rank"},
             "rank_local_ms": round(ms_loc, 6),
             "exchange_ms": round(ms_step - ms_loc, 6),
-            "exchange_ms_gather_to_root": round(ms_root - ms_loc, 6),
+            "exchange_ms_gather_to_root": round(others["gather_to_root"]["exchange_ms"], 6),
+            "plans_beside": others,
             "exchange_note": "exchange_ms: all-gather of Y to every rank (the value's step); "
-                             "exchange_ms_gather_to_root: the reference's semantics, blocks gathered to rank 0 "
+                             "plans_beside.gather_to_root: the reference's semantics, blocks gathered to rank 0 "
                              "only (MPI_Gatherv, SC/...RowWise.cpp:85-87 / MPI_Reduce, ...NonZeroElement.cpp:88); "
-                             "each = (kernel + exchange) - kernel alone, max over ranks",
+                             "reference_rows: the reference's equal-row partition; chunkedC: C row chunks per "
+                             "rank, each chunk's point-to-point all-gatherv started as soon as it is computed; "
+                             "each exchange_ms = (kernel + exchange) - kernel alone, max over ranks",
             "timing": how,
-            "plan": {"create_s_total": round(t_plan, 3), "tiled": st["tiled"], "reuse": round(st["reuse"], 3)},
+            "plan": {"create_s_total": round(t_plan, 3), "tiled": st["tiled"], "reuse": round(st["reuse"], 3),
+                     "partition": args.partition if rows else "reference"},
             "check": {"ok": not bad, "criterion": "Y on every rank vs the 1-GPU sequential plan, device compare "
-                                                  "(bit-identical; NONZERO 1e-6)"},
+                                                  "(bit-identical; NONZERO 1e-6), every all-gather plan"},
             "replicas": {"note": "every rank its own whole problem, no collective (weak scaling)",
                          "ms_per_step": round(ms_rep, 6),
                          "value_GFLOPs": round(world * flops / (ms_rep * 1e-3) / 1e9, 3)},
             "cpu_baseline": None,
         }
         print(json.dumps(out))
-    del copies, reps, P
+    del copies, reps, plans
     comm.close()
     if world > 1:
         dist.destroy_process_group()
@@ -810,16 +851,19 @@ def bench_rank_plans(args, kind: str, K: int, variant: str) -> None:
     X_host = inputs.generateLargeFatVector(n, K)
     prob_bytes = algorithmic_bytes(m, n, nnz, K)
     ncopies = max(1, min(16, math.ceil(args.cold_bytes / prob_bytes) + 1))
-    first, last, off, cnt = D.exchange_plan(V, m, nnz, A.rowPtr, K, p)
+    rowwise = V == smfv.Variant.ROWWISE
+    chunks = args.rank_chunks if rowwise else 1
+    part = args.partition if rowwise else "balanced"
     copies = []
     for c in range(ncopies):
         dA = smfv.DeviceCSR(A, dev)
         dX = torch.from_numpy(X_host).to(dev)
         dY = torch.zeros((m, K), dtype=torch.float64, device=dev)
         plans = [D.DistPlan(None, V, dA, K, to_all=False, rank=(r, p), tiles=args.tiles,
-                            tiled_kernel=args.tiled_kernel) for r in range(p)]
+                            tiled_kernel=args.tiled_kernel, partition=part, chunks=chunks) for r in range(p)]
         copies.append((plans, dX, dY))
     torch.cuda.synchronize()
+    first, last, off, cnt = copies[0][0][0].partition()  # the plans' own partition
     ranks = []
     for r in range(p):
         def step(i, r=r):
@@ -871,6 +915,31 @@ def bench_rank_plans(args, kind: str, K: int, variant: str) -> None:
     loc = [x["local_ms"] for x in ranks]
     flops = 2.0 * nnz * K
     xbytes = [x["exchange_bytes"] for x in ranks]
+    # (r5) the exchange the p-GPU step adds, projected (not measured: no
+    # multi-GPU box): TO_ALL over xGMI's full mesh with point-to-point sends,
+    # every GPU sends its block to each of the p - 1 peers on its own link and
+    # receives theirs, so each link carries one block per direction and the
+    # exchange takes ~ the largest block / the link rate.  The rate is
+    # SURVEY 5's ~153 GB/s per link (--xgmi-gbps), read as per direction;
+    # `half_rate_us` reads it as both directions together.  Chunked (C row
+    # chunks, chunk j's exchange while chunk j + 1 computes): with equal
+    # chunks, max(L / C + E, L + E / C) for rank-local time L and exchange E
+    # (chunk compute taken as L / C: a lower bound, a chunk's plan has its
+    # own fill and drain).
+    link = args.xgmi_gbps * 1e9
+    E_us = max(xbytes) / link * 1e6 if p > 1 else 0.0
+    L_us = max(loc) * 1e3
+    proj = {"assumption": f"xGMI full mesh, {args.xgmi_gbps:.0f} GB/s per link per direction (SURVEY 5, "
+                          "unmeasured here); TO_ALL as point-to-point sends, one block per link per direction",
+            "links_used_per_gpu": p - 1, "bytes_per_link_per_direction_max": max(xbytes) if p > 1 else 0,
+            "bytes_received_per_gpu_max": int(sum(xbytes) - min(xbytes)) if p > 1 else 0,
+            "exchange_us": round(E_us, 3), "exchange_us_half_rate": round(2 * E_us, 3),
+            "rank_local_us_max": round(L_us, 3),
+            "step_us": round(L_us + E_us, 3), "step_us_half_rate": round(L_us + 2 * E_us, 3),
+            "GFLOPs": round(flops / ((L_us + E_us) * 1e-6) / 1e9, 1) if L_us + E_us > 0 else None}
+    if rowwise and p > 1:
+        for C in (2, 4):
+            proj[f"step_us_chunked{C}"] = round(max(L_us / C + E_us, L_us + E_us / C), 3)
     print(json.dumps({
         "projection": f"{p}-GPU decomposition projected on ONE GPU (each rank's share timed alone, in turn); "
                       "not a scaling measurement: no RCCL, no concurrent ranks",
@@ -882,6 +951,8 @@ def bench_rank_plans(args, kind: str, K: int, variant: str) -> None:
         "exchange_bytes_max": max(xbytes), "exchange_bytes_total": int(sum(xbytes)),
         "exchange_note": "bytes a rank's block adds to the exchange (TO_ALL: every rank receives all others' "
                          "blocks: the all-gather moves (p-1)/p of the total into each GPU)",
+        "exchange_projection": proj,
+        "partition": part, "rank_chunks": chunks,
         "ranks": ranks, "tiled_kernel": args.tiled_kernel,
         "check": {"ok": bool(ok), "max_abs_diff": mabs,
                   "criterion": "shares assembled as the exchange would vs the 1-GPU untiled sequential plan "
@@ -1042,6 +1113,17 @@ def main() -> None:
                     help="p > 0: a one-GPU projection of the p-rank decomposition -- every rank's share timed in "
                          "turn through its rank plan (smfv_dist_plan_create_rank); prints a projection line, not "
                          "the headline")
+    ap.add_argument("--partition", default="balanced", choices=["balanced", "reference"],
+                    help="decomposed / --rank-plans ROWWISE: row blocks of equal work (default) or the reference's "
+                         "equal row counts (SC/...RowWise.cpp:26-29)")
+    ap.add_argument("--chunks", type=int, default=2,
+                    help="decomposed ROWWISE: also time the chunked exchange with this many row chunks per rank "
+                         "(SMFV_DIST_CHUNKS; 1 = skip)")
+    ap.add_argument("--rank-chunks", type=int, default=1,
+                    help="--rank-plans ROWWISE: row chunks per rank plan (SMFV_DIST_CHUNKS; each chunk its own plan)")
+    ap.add_argument("--xgmi-gbps", type=float, default=153.0,
+                    help="--rank-plans: xGMI GB/s per link per direction assumed by the exchange projection "
+                         "(SURVEY 5: 7 links of ~153 GB/s per GPU; not measured on this pool)")
     ap.add_argument("--phase-timeout", type=float, default=240.0,
                     help="multi-GPU paths: seconds a phase (RCCL set-up, plans, warm-up, timing, check) may take "
                          "before a diagnostic JSON line and exit status 4 (0 = no watchdog)")

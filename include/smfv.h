@@ -368,6 +368,41 @@ SMFV_API int smfv_comm_bcast(smfv_comm_t comm, void *d_buf, size_t bytes, int ro
 SMFV_API int smfv_dist_plan(int variant, int m, int64_t nnz, const int *h_row_ptr, int K, int p,
                             int *first, int *last, int64_t *offset, int64_t *count);
 
+/* (r5) Distribution options: the high byte of a distributed plan's flags
+ * (the low bits stay smfv_plan_create's SMFV_PLAN_* flags for the rank's
+ * share), and the `dopts` of the *_opts host functions below.
+ *   SMFV_DIST_REFERENCE_ROWS  ROWWISE row blocks by the reference's formula,
+ *        equal row counts (SC/...RowWise.cpp:26-29).  Without it a
+ *        distributed ROWWISE plan cuts the rows into blocks of equal WORK:
+ *        12 B per non-zero + 8K + 4 B per row (the block's CSR and Y bytes),
+ *        so an irregular pattern's ranks finish together.  The result is
+ *        bit-identical either way: each row is summed in CSR order by the one
+ *        rank that owns it.  The Gatherv / all-gatherv exchange takes any
+ *        block sizes (SC/...RowWise.cpp:85-87 does too).
+ *   SMFV_DIST_CHUNKS(c)  ROWWISE, c = 2..7: the rank's block is cut into c
+ *        row chunks of equal work, each a row-block plan of its own; chunk
+ *        j's exchange is issued on the plan's exchange stream as soon as
+ *        chunk j is computed, while chunk j + 1 computes (the exchange of
+ *        one problem overlapped with its own compute).  A chunk's exchange
+ *        is point to point: ncclSend of the chunk to every peer and ncclRecv
+ *        of theirs (TO_ALL, an all-gatherv over the full xGMI mesh) or to the
+ *        root (TO_ROOT, the Gatherv).  0 / 1: one block, one exchange.
+ * Row-partitioned plans (A not replicated) always use the reference rows. */
+#define SMFV_DIST_REFERENCE_ROWS (1 << 24)
+#define SMFV_DIST_CHUNKS(c) (((c) & 7) << 25)
+#define SMFV_DIST_CHUNKS_OF(f) (((f) >> 25) & 7)
+#define SMFV_DIST_OPTS (0xFF << 24)
+/* smfv_dist_plan under distribution options (h_row_ptr needed for
+ * work-balanced ROWWISE blocks; NULL falls back to the reference rows).
+ * smfv_dist_plan(...) = smfv_dist_plan_opts(..., SMFV_DIST_REFERENCE_ROWS). */
+SMFV_API int smfv_dist_plan_opts(int variant, int dopts, int m, int64_t nnz, const int *h_row_ptr, int K, int p,
+                                 int *first, int *last, int64_t *offset, int64_t *count);
+/* ROWWISE under SMFV_DIST_CHUNKS(c): rank `rank`'s chunk boundaries,
+ * chunk j = rows [bounds[j], bounds[j + 1]); bounds holds >= 8 entries,
+ * *nchunks receives c (1 when unchunked: bounds = [first, last + 1]). */
+SMFV_API int smfv_dist_chunk_rows(int variant, int dopts, int m, int64_t nnz, const int *h_row_ptr, int K, int p,
+                                  int rank, int *bounds, int *nchunks);
+
 typedef enum smfv_dist_mode { SMFV_TO_ROOT = 0, SMFV_TO_ALL = 1 } smfv_dist_mode;
 SMFV_API int smfv_dist_workspace_bytes(smfv_comm_t comm, int variant, int m, int64_t nnz,
                                        const int *h_row_ptr, int K, size_t *bytes);
@@ -405,6 +440,11 @@ SMFV_API int smfv_dist_rowpart_spmm_f64(smfv_comm_t comm, int mode, int root, in
 SMFV_API int smfv_dist_exchange_ops(int variant, int mode, int root, int m, int64_t nnz,
                                     const int *h_row_ptr, int K, int p, int rank, int *kinds, int *peers,
                                     int64_t *offsets, int64_t *counts, int *nops);
+/* (r5) The same under distribution options: the ops of chunk `chunk` (0 when
+ * unchunked); a chunked plan runs chunk j's ops after chunk j's compute. */
+SMFV_API int smfv_dist_exchange_ops_opts(int variant, int dopts, int mode, int root, int m, int64_t nnz,
+                                         const int *h_row_ptr, int K, int p, int rank, int chunk, int *kinds,
+                                         int *peers, int64_t *offsets, int64_t *counts, int *nops);
 /* Runs an exchange schedule (ops as smfv_dist_exchange_ops returns them, or
  * any list of the same form) on `comm` over the device buffer d_buf:
  * ncclAllGather alone, else one ncclGroupStart / ncclGroupEnd around the
@@ -448,6 +488,11 @@ SMFV_API int smfv_dist_plan_create_rank(smfv_dist_plan_t *plan, int p, int rank,
  * compact row blocks, at smfv_dist_plan's offset / count) and its size in
  * doubles; NULL / 0 for ROWWISE, whose exchange runs in Y. */
 SMFV_API int smfv_dist_plan_exchange_buffer(smfv_dist_plan_t plan, double **d_buf, int64_t *doubles);
+/* (r5) The partition the plan was created with (p entries each, as
+ * smfv_dist_plan_opts returns them) and its p, rank and chunks per rank. */
+SMFV_API int smfv_dist_plan_partition(smfv_dist_plan_t plan, int *first, int *last, int64_t *offset,
+                                      int64_t *count);
+SMFV_API int smfv_dist_plan_shape(smfv_dist_plan_t plan, int *p, int *rank, int *chunks);
 SMFV_API int smfv_dist_plan_bind_values(smfv_dist_plan_t plan, const double *d_values, void *stream);
 SMFV_API int smfv_dist_plan_execute(smfv_dist_plan_t plan, const int *d_row_ptr, const int *d_col_idx,
                                     const double *d_values, const double *d_X, double *d_Y, void *stream);

@@ -97,6 +97,12 @@ _SIGS = {
                                            c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "smfv_dist_exchange_ops": (c_int, [c_int, c_int, c_int, c_int, c_int64, _PI, c_int, c_int, c_int, _PI, _PI,
                                        _PI64, _PI64, _PI]),
+    "smfv_dist_plan_opts": (c_int, [c_int, c_int, c_int, c_int64, _PI, c_int, c_int, _PI, _PI, _PI64, _PI64]),
+    "smfv_dist_chunk_rows": (c_int, [c_int, c_int, c_int, c_int64, _PI, c_int, c_int, c_int, _PI, _PI]),
+    "smfv_dist_exchange_ops_opts": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int64, _PI, c_int, c_int, c_int,
+                                            c_int, _PI, _PI, _PI64, _PI64, _PI]),
+    "smfv_dist_plan_partition": (c_int, [c_void_p, _PI, _PI, _PI64, _PI64]),
+    "smfv_dist_plan_shape": (c_int, [c_void_p, _PI, _PI, _PI]),
     "smfv_dist_plan_create": (c_int, [POINTER(c_void_p), c_void_p, c_int, c_int, c_int, c_int, c_int, c_int64,
                                       _PI, _PI, c_int, c_int]),
     "smfv_dist_plan_create_rowpart": (c_int, [POINTER(c_void_p), c_void_p, c_int, c_int, c_int, c_int, _PI, _PI,

@@ -181,25 +181,109 @@ SMFV_API int smfv_dist_plan(int variant, int m, int64_t nnz, const int *h_row_pt
 }
 
 namespace {
+// (r5) Cuts of rows [lo, hi) into c pieces of equal work, work(row i) =
+// 12 B per non-zero + (8K + 4) B (its CSR and Y bytes): cut j is the first
+// row i with W(i) >= W(lo) + (W(hi) - W(lo)) * j / c, W(i) = 12 rp[i] +
+// (8K + 4) i.  Integer arithmetic only, so every rank computes the same
+// cuts.  Without row_ptr: equal row counts.  cut[0] = lo, cut[c] = hi.
+void work_cuts(const int *rp, int K, int lo, int hi, int c, int *cut)
+{
+    const int64_t per_row = 8 * (int64_t)K + 4;
+    auto W = [&](int i) -> int64_t { return 12 * (int64_t)rp[i] + per_row * (int64_t)i; };
+    cut[0] = lo;
+    cut[c] = hi;
+    for (int j = 1; j < c; ++j) {
+        if (!rp) {
+            cut[j] = lo + (int)((int64_t)(hi - lo) * j / c);
+            continue;
+        }
+        const __int128 span = (__int128)(W(hi) - W(lo));
+        const int64_t target = W(lo) + (int64_t)(span * j / c);
+        int a = std::max(lo, cut[j - 1]), b = hi;  // first i in [a, b] with W(i) >= target
+        while (a < b) {
+            const int mid = a + (b - a) / 2;
+            if (W(mid) >= target) b = mid; else a = mid + 1;
+        }
+        cut[j] = a;
+    }
+}
+}  // namespace
+
+SMFV_API int smfv_dist_plan_opts(int variant, int dopts, int m, int64_t nnz, const int *h_row_ptr, int K, int p,
+                                 int *first, int *last, int64_t *offset, int64_t *count)
+{
+    const bool rows = variant == SMFV_ROWWISE || variant == SMFV_SEQUENTIAL;
+    if (!rows || (dopts & SMFV_DIST_REFERENCE_ROWS) || !h_row_ptr)
+        return smfv_dist_plan(variant, m, nnz, h_row_ptr, K, p, first, last, offset, count);
+    SMFV_REQUIRE(m >= 0 && K >= 0 && p > 0, "bad argument");
+    SMFV_REQUIRE(first && last && offset && count, "null output array");
+    std::vector<int> cut((size_t)p + 1);
+    work_cuts(h_row_ptr, K, 0, m, p, cut.data());
+    for (int r = 0; r < p; ++r) {
+        first[r] = cut[r];
+        last[r] = cut[r + 1] - 1;
+        offset[r] = (int64_t)cut[r] * K;
+        count[r] = (int64_t)(cut[r + 1] - cut[r]) * K;
+    }
+    return SMFV_OK;
+}
+
+namespace {
 struct Plan {
     std::vector<int> first, last;
     std::vector<int64_t> offset, count;
     int64_t total = 0;  // doubles in the exchange buffer
+    int K = 0;
+    int chunks = 1;         // (r5) ROWWISE: row chunks per rank, each exchanged on its own
+    std::vector<int> cb;    // chunked: rank r's chunk j = rows [cb[r (chunks + 1) + j], cb[r (chunks + 1) + j + 1])
 };
-int make_plan(int variant, int m, int64_t nnz, const int *h_row_ptr, int K, int p, Plan &P)
+// (the plain host functions and the plan-less smfv_dist_spmm_f64 keep the
+// reference's partition; distributed plans pass their own options)
+int make_plan(int variant, int m, int64_t nnz, const int *h_row_ptr, int K, int p, Plan &P,
+              int dopts = SMFV_DIST_REFERENCE_ROWS)
 {
     P.first.assign(p, 0);
     P.last.assign(p, -1);
     P.offset.assign(p, 0);
     P.count.assign(p, 0);
-    int rc = smfv_dist_plan(variant, m, nnz, h_row_ptr, K, p, P.first.data(), P.last.data(),
-                            P.offset.data(), P.count.data());
+    P.K = K;
+    int rc = smfv_dist_plan_opts(variant, dopts, m, nnz, h_row_ptr, K, p, P.first.data(), P.last.data(),
+                                 P.offset.data(), P.count.data());
     if (rc) return rc;
     P.total = 0;
     for (int r = 0; r < p; ++r) P.total = std::max(P.total, P.offset[r] + P.count[r]);
+    const int c = SMFV_DIST_CHUNKS_OF(dopts);
+    P.chunks = 1;
+    P.cb.clear();
+    if (c > 1) {
+        if (variant != SMFV_ROWWISE && variant != SMFV_SEQUENTIAL) {
+            set_error("SMFV_DIST_CHUNKS applies to ROWWISE (variant %d)", variant);
+            return SMFV_ERR_INVALID;
+        }
+        P.chunks = c;
+        P.cb.assign((size_t)p * (c + 1), 0);
+        for (int r = 0; r < p; ++r) work_cuts(h_row_ptr, K, P.first[r], P.last[r] + 1, c, &P.cb[(size_t)r * (c + 1)]);
+    }
     return SMFV_OK;
 }
 }  // namespace
+
+SMFV_API int smfv_dist_chunk_rows(int variant, int dopts, int m, int64_t nnz, const int *h_row_ptr, int K, int p,
+                                  int rank, int *bounds, int *nchunks)
+{
+    SMFV_REQUIRE(bounds && nchunks && p > 0 && rank >= 0 && rank < p, "bad argument");
+    Plan P;
+    int rc = make_plan(variant, m, nnz, h_row_ptr, K, p, P, dopts);
+    if (rc) return rc;
+    *nchunks = P.chunks;
+    if (P.chunks == 1) {
+        bounds[0] = P.first[rank];
+        bounds[1] = P.last[rank] + 1;
+    } else {
+        for (int j = 0; j <= P.chunks; ++j) bounds[j] = P.cb[(size_t)rank * (P.chunks + 1) + j];
+    }
+    return SMFV_OK;
+}
 
 SMFV_API int smfv_dist_workspace_bytes(smfv_comm_t comm, int variant, int m, int64_t nnz,
                                        const int *h_row_ptr, int K, size_t *bytes)
@@ -240,10 +324,37 @@ struct ExOp {
 };
 
 static std::vector<ExOp> exchange_schedule(const Plan &P, int p, int rank, bool may_be_equal, bool to_all,
-                                           int root)
+                                           int root, int chunk = 0)
 {
     std::vector<ExOp> ops;
     if (p <= 1) return ops;
+    if (P.chunks > 1) {
+        // (r5) chunk `chunk` of every rank's row block, point to point: every
+        // rank sends its chunk to each peer (TO_ALL) or to the root, and
+        // receives theirs -- one group; over xGMI's full mesh each link
+        // carries one chunk per direction
+        const int C1 = P.chunks + 1;
+        auto blk = [&](int r, int64_t &off, int64_t &cnt) {
+            const int s = P.cb[(size_t)r * C1 + chunk], e = P.cb[(size_t)r * C1 + chunk + 1];
+            off = (int64_t)s * P.K;
+            cnt = (int64_t)(e - s) * P.K;
+        };
+        int64_t off, cnt;
+        blk(rank, off, cnt);
+        if (to_all || rank != root) {
+            if (cnt > 0)
+                for (int r = 0; r < p; ++r)
+                    if (r != rank && (to_all || r == root)) ops.push_back({SMFV_EX_SEND, r, off, cnt});
+        }
+        if (to_all || rank == root) {
+            for (int r = 0; r < p; ++r) {
+                if (r == rank) continue;
+                blk(r, off, cnt);
+                if (cnt > 0) ops.push_back({SMFV_EX_RECV, r, off, cnt});
+            }
+        }
+        return ops;
+    }
     bool equal = may_be_equal;
     for (int r = 1; r < p && equal; ++r)
         equal = P.count[r] == P.count[0] && P.offset[r] == P.offset[0] + r * P.count[0];
@@ -321,6 +432,28 @@ SMFV_API int smfv_dist_exchange_ops(int variant, int mode, int root, int m, int6
     int rc = make_plan(variant, m, nnz, h_row_ptr, K, p, P);
     if (rc) return rc;
     const auto ops = exchange_schedule(P, p, rank, variant != SMFV_NONZERO, mode == SMFV_TO_ALL, root);
+    for (size_t i = 0; i < ops.size(); ++i) {
+        kinds[i] = ops[i].kind;
+        peers[i] = ops[i].peer;
+        offsets[i] = ops[i].offset;
+        counts[i] = ops[i].count;
+    }
+    *nops = (int)ops.size();
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_dist_exchange_ops_opts(int variant, int dopts, int mode, int root, int m, int64_t nnz,
+                                         const int *h_row_ptr, int K, int p, int rank, int chunk, int *kinds,
+                                         int *peers, int64_t *offsets, int64_t *counts, int *nops)
+{
+    SMFV_REQUIRE(kinds && peers && offsets && counts && nops, "null output array");
+    SMFV_REQUIRE(p > 0 && rank >= 0 && rank < p && root >= 0 && root < p, "bad rank / root");
+    SMFV_REQUIRE(mode == SMFV_TO_ROOT || mode == SMFV_TO_ALL, "bad mode %d", mode);
+    Plan P;
+    int rc = make_plan(variant, m, nnz, h_row_ptr, K, p, P, dopts);
+    if (rc) return rc;
+    SMFV_REQUIRE(chunk >= 0 && chunk < P.chunks, "chunk %d of %d", chunk, P.chunks);
+    const auto ops = exchange_schedule(P, p, rank, variant != SMFV_NONZERO, mode == SMFV_TO_ALL, root, chunk);
     for (size_t i = 0; i < ops.size(); ++i) {
         kinds[i] = ops[i].kind;
         peers[i] = ops[i].peer;
@@ -449,16 +582,45 @@ struct smfv_dist_plan_s {
     std::vector<ExOp> ops;
     smfv_plan_t local = nullptr;  // this rank's share as a single-device plan
     double *xbuf = nullptr;       // exchange buffer (COLUMNWISE panels / NONZERO row blocks)
+    // (r5) chunked ROWWISE (SMFV_DIST_CHUNKS): one row-block plan and one
+    // exchange per chunk; chunk j's exchange runs on xst after chunk j's
+    // compute (event cev[j]) while chunk j + 1 computes; xdone joins back
+    std::vector<smfv_plan_t> cplans;
+    std::vector<std::vector<ExOp>> cops;
+    hipStream_t xst = nullptr;
+    std::vector<hipEvent_t> cev;
+    hipEvent_t xdone = nullptr;
     ~smfv_dist_plan_s()
     {
         if (local) smfv_plan_destroy(local);
+        for (smfv_plan_t c : cplans)
+            if (c) smfv_plan_destroy(c);
+        for (hipEvent_t e : cev) (void)hipEventDestroy(e);
+        if (xdone) (void)hipEventDestroy(xdone);
+        if (xst) (void)hipStreamDestroy(xst);
         if (xbuf) (void)hipFree(xbuf);
     }
+    int chunk_begin(int j) const { return P.cb[(size_t)rank * (P.chunks + 1) + j]; }
 };
 
 static int dist_plan_finish(smfv_dist_plan_s *d, smfv_dist_plan_t *out)
 {
     d->ops = exchange_schedule(d->P, d->p, d->rank, d->variant != SMFV_NONZERO, d->mode == SMFV_TO_ALL, d->root);
+    if (d->P.chunks > 1) {
+        d->cops.clear();
+        for (int j = 0; j < d->P.chunks; ++j)
+            d->cops.push_back(exchange_schedule(d->P, d->p, d->rank, true, d->mode == SMFV_TO_ALL, d->root, j));
+        d->cev.assign((size_t)d->P.chunks, nullptr);
+        hipError_t e = hipStreamCreateWithFlags(&d->xst, hipStreamNonBlocking);
+        for (int j = 0; e == hipSuccess && j < d->P.chunks; ++j)
+            e = hipEventCreateWithFlags(&d->cev[(size_t)j], hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&d->xdone, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            set_error("exchange stream / events: %s", hipGetErrorString(e));
+            delete d;
+            return SMFV_ERR_HIP;
+        }
+    }
     if (d->variant == SMFV_COLUMNWISE || d->variant == SMFV_NONZERO) {
         const size_t b = std::max<size_t>((size_t)d->P.total, 1) * sizeof(double);
         hipError_t e = hipMalloc(reinterpret_cast<void **>(&d->xbuf), b);
@@ -493,11 +655,21 @@ static int dist_plan_create(smfv_dist_plan_t *out, smfv_comm_t comm, int p, int 
     d->m = m;
     d->n = n;
     d->K = K;
-    int rc = make_plan(d->variant, m, nnz, h_row_ptr, K, p, d->P);
+    const int dopts = flags & SMFV_DIST_OPTS;
+    flags &= ~SMFV_DIST_OPTS;
+    int rc = make_plan(d->variant, m, nnz, h_row_ptr, K, p, d->P, dopts);
     if (!rc) {
         const int f = d->P.first[rank], l = d->P.last[rank];
         switch (d->variant) {
         case SMFV_ROWWISE:  // rows [f, l] (SC/...RowWise.cpp:26-50)
+            if (d->P.chunks > 1) {  // (r5) one row-block plan per chunk (empty chunks: none)
+                d->cplans.assign((size_t)d->P.chunks, nullptr);
+                for (int j = 0; !rc && j < d->P.chunks; ++j)
+                    if (d->chunk_begin(j + 1) > d->chunk_begin(j))
+                        rc = smfv_plan_create_rows(&d->cplans[(size_t)j], SMFV_ROWWISE, d->chunk_begin(j),
+                                                   d->chunk_begin(j + 1), n, h_row_ptr, h_col_idx, K, flags);
+                break;
+            }
             rc = smfv_plan_create_rows(&d->local, SMFV_ROWWISE, f, l + 1, n, h_row_ptr, h_col_idx, K, flags);
             break;
         case SMFV_COLUMNWISE:  // all rows, K columns [f, l] (SC/...ColumnWise.cpp:25-48)
@@ -553,6 +725,8 @@ SMFV_API int smfv_dist_plan_create_rowpart(smfv_dist_plan_t *out, smfv_comm_t co
     d->m = m;
     d->n = n;
     d->K = K;
+    // (the rows are given: the reference partition, one block, SMFV_DIST_* ignored)
+    flags &= ~SMFV_DIST_OPTS;
     int rc = make_plan(SMFV_ROWWISE, m, 0, nullptr, K, comm->nranks, d->P);
     const int first = d->P.first[comm->rank];
     const int mloc = d->P.last[comm->rank] - first + 1;
@@ -576,9 +750,38 @@ SMFV_API int smfv_dist_plan_exchange_buffer(smfv_dist_plan_t d, double **d_buf, 
     return SMFV_OK;
 }
 
+SMFV_API int smfv_dist_plan_partition(smfv_dist_plan_t d, int *first, int *last, int64_t *offset, int64_t *count)
+{
+    SMFV_REQUIRE(d && first && last && offset && count, "null argument");
+    for (int r = 0; r < d->p; ++r) {
+        first[r] = d->P.first[r];
+        last[r] = d->P.last[r];
+        offset[r] = d->P.offset[r];
+        count[r] = d->P.count[r];
+    }
+    return SMFV_OK;
+}
+
+SMFV_API int smfv_dist_plan_shape(smfv_dist_plan_t d, int *p, int *rank, int *chunks)
+{
+    SMFV_REQUIRE(d && p && rank && chunks, "null argument");
+    *p = d->p;
+    *rank = d->rank;
+    *chunks = d->P.chunks;
+    return SMFV_OK;
+}
+
 SMFV_API int smfv_dist_plan_bind_values(smfv_dist_plan_t d, const double *d_values, void *stream)
 {
     SMFV_REQUIRE(d, "null plan");
+    if (d->P.chunks > 1) {
+        for (smfv_plan_t c : d->cplans)
+            if (c) {
+                int rc = smfv_plan_bind_values(c, d_values, stream);
+                if (rc) return rc;
+            }
+        return SMFV_OK;
+    }
     return smfv_plan_bind_values(d->local, d_values, stream);
 }
 
@@ -591,6 +794,15 @@ SMFV_API int smfv_dist_plan_execute_local(smfv_dist_plan_t d, const int *d_row_p
     const int f = d->P.first[rank], l = d->P.last[rank];
     switch (d->variant) {
     case SMFV_ROWWISE:  // in place: this rank's rows of Y
+        if (d->P.chunks > 1) {
+            for (int j = 0; j < d->P.chunks; ++j)
+                if (d->cplans[(size_t)j]) {
+                    int rc = smfv_plan_execute(d->cplans[(size_t)j], d_row_ptr, d_col_idx, d_values, d_X, K,
+                                               d_Y + (int64_t)d->chunk_begin(j) * K, K, stream);
+                    if (rc) return rc;
+                }
+            return SMFV_OK;
+        }
         return smfv_plan_execute(d->local, d_row_ptr, d_col_idx, d_values, d_X, K, d_Y + d->P.offset[rank], K,
                                  stream);
     case SMFV_COLUMNWISE: {  // [m x kc] panel from the X column window
@@ -611,6 +823,13 @@ SMFV_API int smfv_dist_plan_exchange(smfv_dist_plan_t d, double *d_Y, void *stre
     SMFV_REQUIRE(d, "null plan");
     hipStream_t st = smfv::as_stream(stream);
     double *buf = d->variant == SMFV_ROWWISE ? d_Y : d->xbuf;
+    if (d->P.chunks > 1) {  // the chunks' exchanges back to back (the exchange alone)
+        for (const auto &ops : d->cops) {
+            int rc = run_exchange(d->comm, ops, buf, st);
+            if (rc) return rc;
+        }
+        return SMFV_OK;
+    }
     int rc = run_exchange(d->comm, d->ops, buf, st);
     if (rc) return rc;
     const int p = d->p;
@@ -622,9 +841,42 @@ SMFV_API int smfv_dist_plan_exchange(smfv_dist_plan_t d, double *d_Y, void *stre
     return SMFV_OK;
 }
 
+#define SMFV_HIP_D(call)                                                                    \
+    do {                                                                                    \
+        hipError_t e_ = (call);                                                             \
+        if (e_ != hipSuccess) {                                                             \
+            set_error("%s: %s", #call, hipGetErrorString(e_));                              \
+            return SMFV_ERR_HIP;                                                            \
+        }                                                                                   \
+    } while (0)
+
 SMFV_API int smfv_dist_plan_execute(smfv_dist_plan_t d, const int *d_row_ptr, const int *d_col_idx,
                                     const double *d_values, const double *d_X, double *d_Y, void *stream)
 {
+    SMFV_REQUIRE(d, "null plan");
+    if (d->P.chunks > 1) {
+        // (r5) chunk j computes on `stream`; its exchange waits for it on the
+        // plan's exchange stream and runs while chunk j + 1 computes; the
+        // caller's stream waits for the last exchange.  (A capturing stream
+        // forks to the exchange stream and joins back: graph-capturable.)
+        SMFV_REQUIRE(d_Y || d->m == 0 || d->K == 0, "null Y");
+        hipStream_t st = smfv::as_stream(stream);
+        const int K = d->K;
+        for (int j = 0; j < d->P.chunks; ++j) {
+            if (d->cplans[(size_t)j]) {
+                int rc = smfv_plan_execute(d->cplans[(size_t)j], d_row_ptr, d_col_idx, d_values, d_X, K,
+                                           d_Y + (int64_t)d->chunk_begin(j) * K, K, stream);
+                if (rc) return rc;
+            }
+            SMFV_HIP_D(hipEventRecord(d->cev[(size_t)j], st));
+            SMFV_HIP_D(hipStreamWaitEvent(d->xst, d->cev[(size_t)j], 0));
+            int rc = run_exchange(d->comm, d->cops[(size_t)j], d_Y, d->xst);
+            if (rc) return rc;
+        }
+        SMFV_HIP_D(hipEventRecord(d->xdone, d->xst));
+        SMFV_HIP_D(hipStreamWaitEvent(st, d->xdone, 0));
+        return SMFV_OK;
+    }
     int rc = smfv_dist_plan_execute_local(d, d_row_ptr, d_col_idx, d_values, d_X, d_Y, stream);
     return rc ? rc : smfv_dist_plan_exchange(d, d_Y, stream);
 }
@@ -632,6 +884,31 @@ SMFV_API int smfv_dist_plan_execute(smfv_dist_plan_t d, const int *d_row_ptr, co
 SMFV_API int smfv_dist_plan_stats(smfv_dist_plan_t d, double out[SMFV_PLAN_STATS])
 {
     SMFV_REQUIRE(d, "null plan");
+    if (d->P.chunks > 1) {
+        // the first chunk's stats; counts summed over the chunks (tiles, staged
+        // rows, device bytes, direct rows, analysis time, snapshot entries),
+        // re-use weighted by staged rows, tiled only if every chunk is
+        for (int i = 0; i < SMFV_PLAN_STATS; ++i) out[i] = 0.0;
+        bool first = true;
+        double reuse_w = 0.0;
+        for (smfv_plan_t c : d->cplans) {
+            if (!c) continue;
+            double o[SMFV_PLAN_STATS];
+            int rc = smfv_plan_stats(c, o);
+            if (rc) return rc;
+            if (first) {
+                for (int i = 0; i < SMFV_PLAN_STATS; ++i) out[i] = o[i];
+                for (int i : {1, 2, 4, 5, 8, 9}) out[i] = 0.0;
+                first = false;
+            }
+            out[0] = out[0] && o[0];
+            for (int i : {1, 2, 4, 5, 8, 9}) out[i] += o[i];
+            reuse_w += o[3] * o[2];
+        }
+        out[3] = out[2] > 0 ? reuse_w / out[2] : 0.0;
+        out[6] = d->P.first[d->rank];
+        return SMFV_OK;
+    }
     return smfv_plan_stats(d->local, out);
 }
 

@@ -24,22 +24,53 @@ from .engine import DeviceCSR, Variant, stream_handle
 
 UNIQUE_ID_BYTES = 128
 TO_ROOT, TO_ALL = 0, 1
+# (r5) distribution options (include/smfv.h SMFV_DIST_*), the high byte of a
+# distributed plan's flags
+REFERENCE_ROWS = 1 << 24
 
 
-def exchange_plan(variant: int, m: int, nnz: int, row_ptr: np.ndarray | None, K: int, p: int):
-    """Native smfv_dist_plan: per-rank (first, last, offset, count) arrays."""
+def dist_opts(partition: str = "balanced", chunks: int = 1) -> int:
+    """SMFV_DIST_* bits: ROWWISE row blocks of equal work ("balanced", the
+    distributed plans' default) or the reference's equal row counts
+    ("reference", SC/...RowWise.cpp:26-29); `chunks` row chunks per rank,
+    each exchanged as soon as it is computed (SMFV_DIST_CHUNKS)."""
+    if partition not in ("balanced", "reference") or not 1 <= chunks <= 7:
+        raise ValueError(f"partition {partition!r}, chunks {chunks}")
+    return (REFERENCE_ROWS if partition == "reference" else 0) | ((chunks & 7) << 25 if chunks > 1 else 0)
+
+
+def _rp(row_ptr):
+    if row_ptr is None:
+        return None, None
+    row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
+    return row_ptr, row_ptr.ctypes.data_as(POINTER(c_int))
+
+
+def exchange_plan(variant: int, m: int, nnz: int, row_ptr: np.ndarray | None, K: int, p: int,
+                  dopts: int = REFERENCE_ROWS):
+    """Native smfv_dist_plan_opts: per-rank (first, last, offset, count)
+    arrays; by default the reference's partition (smfv_dist_plan)."""
     first = np.zeros(p, dtype=np.int32)
     last = np.zeros(p, dtype=np.int32)
     offset = np.zeros(p, dtype=np.int64)
     count = np.zeros(p, dtype=np.int64)
-    rp = None
-    if row_ptr is not None:
-        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
-        rp = row_ptr.ctypes.data_as(POINTER(c_int))
-    call("smfv_dist_plan", int(variant), m, nnz, rp, K, p,
+    keep, rp = _rp(row_ptr)
+    call("smfv_dist_plan_opts", int(variant), int(dopts), m, nnz, rp, K, p,
          first.ctypes.data_as(POINTER(c_int)), last.ctypes.data_as(POINTER(c_int)),
          offset.ctypes.data_as(POINTER(c_int64)), count.ctypes.data_as(POINTER(c_int64)))
     return first, last, offset, count
+
+
+def chunk_rows(variant: int, dopts: int, m: int, nnz: int, row_ptr: np.ndarray | None, K: int, p: int,
+               rank: int) -> list[int]:
+    """Native smfv_dist_chunk_rows: rank's chunk boundaries (chunk j = rows
+    [b[j], b[j + 1]))."""
+    b = np.zeros(8, dtype=np.int32)
+    n = c_int(0)
+    keep, rp = _rp(row_ptr)
+    call("smfv_dist_chunk_rows", int(variant), int(dopts), m, nnz, rp, K, p, rank,
+         b.ctypes.data_as(POINTER(c_int)), byref(n))
+    return [int(v) for v in b[:n.value + 1]]
 
 
 class Communicator:
@@ -96,21 +127,19 @@ EX_ALLGATHER, EX_BCAST, EX_SEND, EX_RECV = 1, 2, 3, 4  # SMFV_EX_*
 
 
 def exchange_ops(variant: int, mode: int, root: int, m: int, nnz: int, row_ptr: np.ndarray | None, K: int,
-                 p: int, rank: int) -> list[tuple[int, int, int, int]]:
-    """Native smfv_dist_exchange_ops: the exchange step of `rank` as a list
-    of (kind, peer, offset, count) -- the schedule the RCCL path runs."""
+                 p: int, rank: int, dopts: int = REFERENCE_ROWS, chunk: int = 0) -> list[tuple[int, int, int, int]]:
+    """Native smfv_dist_exchange_ops_opts: the exchange step of `rank` (of
+    chunk `chunk` under SMFV_DIST_CHUNKS) as a list of (kind, peer, offset,
+    count) -- the schedule the RCCL path runs, in one group."""
     cap = 2 * p + 2
     kinds = np.zeros(cap, np.int32)
     peers = np.zeros(cap, np.int32)
     offs = np.zeros(cap, np.int64)
     cnts = np.zeros(cap, np.int64)
     n = c_int(0)
-    rp = None
-    if row_ptr is not None:
-        row_ptr = np.ascontiguousarray(row_ptr, dtype=np.int32)
-        rp = row_ptr.ctypes.data_as(POINTER(c_int))
-    call("smfv_dist_exchange_ops", int(variant), int(mode), int(root), m, nnz, rp, K, p, rank,
-         kinds.ctypes.data_as(POINTER(c_int)), peers.ctypes.data_as(POINTER(c_int)),
+    keep, rp = _rp(row_ptr)
+    call("smfv_dist_exchange_ops_opts", int(variant), int(dopts), int(mode), int(root), m, nnz, rp, K, p, rank,
+         int(chunk), kinds.ctypes.data_as(POINTER(c_int)), peers.ctypes.data_as(POINTER(c_int)),
          offs.ctypes.data_as(POINTER(c_int64)), cnts.ctypes.data_as(POINTER(c_int64)), byref(n))
     return [(int(kinds[i]), int(peers[i]), int(offs[i]), int(cnts[i])) for i in range(n.value)]
 
@@ -143,7 +172,8 @@ class DistPlan:
 
     def __init__(self, comm: Communicator | None, variant: int, A: DeviceCSR, K: int, to_all: bool,
                  root: int = 0, tiles: str = "auto", rowpart: bool = False, m: int | None = None,
-                 stream=None, rank: tuple[int, int] | None = None, fma: bool = False, tiled_kernel: str = "auto"):
+                 stream=None, rank: tuple[int, int] | None = None, fma: bool = False, tiled_kernel: str = "auto",
+                 partition: str = "balanced", chunks: int = 1):
         self.comm, self.variant, self.A, self.K = comm, Variant(variant), A, K
         self.mode = TO_ALL if to_all else TO_ROOT
         self.root = root
@@ -153,6 +183,9 @@ class DistPlan:
         # the rank share's tiled-kernel geometry (SpmmPlan's tiled_kernel; A/B)
         flags |= {"auto": 0, "ws1": PLAN_WS | PLAN_WS_GEOM1, "ws2": PLAN_WS | PLAN_WS_GEOM2,
                   "ws3": PLAN_WS | PLAN_WS_GEOM3}[tiled_kernel]
+        # (r5) ROWWISE blocks of equal work by default ("reference": equal rows);
+        # chunks > 1: per-chunk exchanges overlapped with the next chunk's compute
+        flags |= dist_opts(partition, chunks)
         ip = POINTER(c_int)
         self._h = c_void_p()
         if comm is None:
@@ -213,6 +246,25 @@ class DistPlan:
         addr = ctypes.cast(ptr, c_void_p).value
         # a non-owning view of the plan's device buffer (the plan outlives it)
         return _device_view(addr, n.value, self.A.device, owner=self)
+
+    def partition(self):
+        """(first, last, offset, count) per rank: the partition this plan was
+        created with (smfv_dist_plan_partition)."""
+        p, r, c = self.shape()
+        first = np.zeros(p, dtype=np.int32)
+        last = np.zeros(p, dtype=np.int32)
+        offset = np.zeros(p, dtype=np.int64)
+        count = np.zeros(p, dtype=np.int64)
+        call("smfv_dist_plan_partition", self._h, first.ctypes.data_as(POINTER(c_int)),
+             last.ctypes.data_as(POINTER(c_int)), offset.ctypes.data_as(POINTER(c_int64)),
+             count.ctypes.data_as(POINTER(c_int64)))
+        return first, last, offset, count
+
+    def shape(self) -> tuple[int, int, int]:
+        """(p, rank, chunks per rank) of the plan."""
+        p, r, c = c_int(0), c_int(0), c_int(0)
+        call("smfv_dist_plan_shape", self._h, byref(p), byref(r), byref(c))
+        return p.value, r.value, c.value
 
     def stats(self) -> dict:
         from .engine import PLAN_STATS

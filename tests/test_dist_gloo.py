@@ -44,8 +44,27 @@ def _local_part(variant, A, X, first, last, rank, p):
 
 
 def run_ops(ops, xbuf: torch.Tensor, rank: int, p: int) -> None:
-    """Replay a native exchange schedule over torch.distributed (gloo)."""
+    """Replay a native exchange schedule over torch.distributed (gloo).  The
+    ops of one schedule form one RCCL group (ncclGroupStart / End): a
+    schedule of point-to-point ops (the chunked all-gatherv sends AND
+    receives on every rank) is replayed as isend / irecv completed together,
+    as the group completes them."""
     from sparsematrixmultiplicationmpi_amd.dist import EX_ALLGATHER, EX_BCAST, EX_RECV, EX_SEND
+    if ops and all(k in (EX_SEND, EX_RECV) for k, _, _, _ in ops) and \
+            any(k == EX_RECV for k, _, _, _ in ops) and any(k == EX_SEND for k, _, _, _ in ops):
+        reqs, landing = [], []
+        for kind, peer, off, cnt in ops:
+            if kind == EX_SEND:
+                reqs.append(dist.isend(xbuf[off:off + cnt].clone(), dst=peer))
+            else:
+                blk = torch.zeros(cnt, dtype=torch.float64)
+                reqs.append(dist.irecv(blk, src=peer))
+                landing.append((off, cnt, blk))
+        for rq in reqs:
+            rq.wait()
+        for off, cnt, blk in landing:
+            xbuf[off:off + cnt] = blk
+        return
     for kind, peer, off, cnt in ops:
         if kind == EX_ALLGATHER:
             base = off - rank * cnt
@@ -275,3 +294,67 @@ def test_gloo_reference_degenerate_p8():
         pr.join(timeout=60)
     for rank, ok, info in res:
         assert ok, (rank, info)
+
+
+def _chunked_worker(rank, p, port, partition, chunks, q):
+    """(r5) The work-balanced ROWWISE partition and the chunked exchange
+    (SMFV_DIST_CHUNKS): rank r's block [first, last] of the native balanced
+    (or reference) partition, computed by the oracle, then the native
+    per-chunk schedules run chunk after chunk -- point-to-point sends and
+    receives of each chunk to every peer (TO_ALL) or the root (TO_ROOT) --
+    must assemble the reference's sequential Y bit for bit."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=p)
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import sparsematrixmultiplicationmpi_amd as smfv
+        from sparsematrixmultiplicationmpi_amd.dist import TO_ALL, chunk_rows, dist_opts, exchange_ops, exchange_plan
+        from oracle import oracle
+
+        A = smfv.gen_random_rows(1500, 900, 8, 2.0, 300, 37)
+        K = 5
+        X = np.random.default_rng(37).uniform(-1, 1, (A.numCols, K))
+        m, nnz = A.numRows, A.nnz
+        dopts = dist_opts(partition, chunks)
+        first, last, off, cnt = exchange_plan(1, m, nnz, A.rowPtr, K, p, dopts)
+        # chunk boundaries tile the rank's block
+        b = chunk_rows(1, dopts, m, nnz, A.rowPtr, K, p, rank)
+        assert b[0] == first[rank] and b[-1] == last[rank] + 1 and len(b) == chunks + 1 and b == sorted(b)
+        Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+        out = []
+        for mode in (0, 1):
+            root = p - 1
+            xbuf = torch.full((m * K,), float("nan"), dtype=torch.float64)
+            mine = _local_part(1, A, X, first[rank], last[rank], rank, p)
+            xbuf[off[rank]: off[rank] + cnt[rank]] = torch.from_numpy(mine)
+            nops = 0
+            for j in range(chunks):
+                ops = exchange_ops(1, mode, root, m, nnz, A.rowPtr, K, p, rank, dopts, j)
+                nops += len(ops)
+                run_ops(ops, xbuf, rank, p)
+            if mode != TO_ALL and rank != root:
+                continue
+            Y = xbuf.numpy().reshape(m, K)
+            out.append((mode, bool(np.array_equal(Y.view(np.uint64), Yref.view(np.uint64))), nops))
+        q.put((rank, all(o[1] for o in out), out))
+        dist.destroy_process_group()
+    except Exception as e:  # surface worker failures
+        import traceback
+        q.put((rank, False, traceback.format_exc()[-1500:]))
+
+
+@pytest.mark.parametrize("p,partition,chunks", [(2, "balanced", 2), (3, "balanced", 3), (3, "reference", 2),
+                                                (8, "balanced", 4), (2, "balanced", 1)])
+def test_gloo_chunked_rowwise_exchange(p, partition, chunks):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_chunked_worker, args=(r, p, port, partition, chunks, q)) for r in range(p)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=300) for _ in range(p)]
+    for pr in procs:
+        pr.join(timeout=60)
+    for rank, ok, info in res:
+        assert ok, (p, partition, chunks, rank, info)

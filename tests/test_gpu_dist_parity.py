@@ -96,19 +96,24 @@ def check(variant, g, p, Y):
 
 
 @pytest.mark.parametrize("name,p", CASES)
-@pytest.mark.parametrize("variant", [smfv.Variant.ROWWISE, smfv.Variant.COLUMNWISE, smfv.Variant.NONZERO])
+@pytest.mark.parametrize("variant,partition", [(smfv.Variant.ROWWISE, "reference"), (smfv.Variant.ROWWISE, "balanced"),
+                                               (smfv.Variant.COLUMNWISE, "balanced"),
+                                               (smfv.Variant.NONZERO, "balanced")])
 @pytest.mark.parametrize("tiles", ["auto", "force", "off"])
-def test_rank_plans_vs_reference(gpu, name, p, variant, tiles):
+def test_rank_plans_vs_reference(gpu, name, p, variant, partition, tiles):
     """Every rank's plan (smfv_dist_plan_create_rank) + the native exchange
-    schedule replayed on the device = the reference's result at p ranks."""
+    schedule replayed on the device = the reference's result at p ranks.
+    (r5) ROWWISE under both row partitions: the reference's equal rows and
+    the plans' default equal-work blocks (same bytes: a row is summed by one
+    rank in CSR order either way)."""
     g, A, dA, dX = golden_problem(name, gpu)
     K = dX.shape[1]
     root = p - 1  # a root other than 0 where p > 1
-    first, last, off, cnt = D.exchange_plan(variant, A.numRows, A.nnz, A.rowPtr, K, p)
+    first, last, off, cnt = D.exchange_plan(variant, A.numRows, A.nnz, A.rowPtr, K, p, D.dist_opts(partition))
     Y = torch.full((A.numRows, K), float("nan"), dtype=torch.float64, device=gpu)
     blocks, plans = [], []
     for r in range(p):
-        P = D.DistPlan(None, variant, dA, K, to_all=False, root=root, tiles=tiles, rank=(r, p))
+        P = D.DistPlan(None, variant, dA, K, to_all=False, root=root, tiles=tiles, rank=(r, p), partition=partition)
         plans.append(P)
         P.run_local(dX, Y)
         buf = P.exchange_buffer()

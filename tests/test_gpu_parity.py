@@ -780,6 +780,55 @@ def test_dist_plan_single_rank(gpu):
     comm.close()
 
 
+def test_dist_plan_chunked_single_rank(gpu):
+    """(r5) A chunked ROWWISE distributed plan (SMFV_DIST_CHUNKS: one tiled
+    row-block plan per chunk; each chunk's exchange waits for it on the
+    plan's exchange stream, the caller's stream joins the last) on a
+    one-rank communicator: bit-identical eager and inside a captured
+    hipGraph (the fork to the exchange stream and the join back are
+    captured), under both row partitions, with a values change re-bound."""
+    from sparsematrixmultiplicationmpi_amd import dist as D
+    comm = D.Communicator(0, 1, D.Communicator.new_unique_id())
+    A = smfv.gen_fem27(9000, 14, 14, 0.83, 61)
+    K = 32
+    X = np.random.default_rng(61).uniform(-1, 1, (A.numCols, K))
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    dA = smfv.DeviceCSR(A, gpu)
+    dX = torch.from_numpy(X).to(gpu)
+    for partition in ("balanced", "reference"):
+        for chunks in (2, 3, 7):
+            for to_all in (False, True):
+                P = D.DistPlan(comm, smfv.Variant.ROWWISE, dA, K, to_all, tiles="force", partition=partition,
+                               chunks=chunks)
+                assert P.shape() == (1, 0, chunks) and P.stats()["tiled"]
+                Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+                P.run(dX, Y)
+                torch.cuda.synchronize()
+                assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref)), (partition, chunks, to_all)
+                Y.fill_(np.nan)
+                g = torch.cuda.CUDAGraph()
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    with torch.cuda.graph(g, stream=side):
+                        P.run(dX, Y, stream=side)
+                torch.cuda.current_stream().wait_stream(side)
+                g.replay()
+                torch.cuda.synchronize()
+                assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref)), ("graph", partition, chunks, to_all)
+                del g
+    # values changed in place: the chunk plans re-bind together
+    dA.values.mul_(2.0)
+    A2 = smfv.SparseMatrix(A.values * 2.0, A.colIndices, A.rowPtr, A.numRows, A.numCols)
+    Y2ref = oracle.spmm("sequential", A2.rowPtr, A2.colIndices, A2.values, X)
+    Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+    P.run(dX, Y)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(Y.cpu().numpy()), bits(Y2ref))
+    del P
+    comm.close()
+
+
 def test_columnwise_single_pass_k128(gpu):
     """COLUMNWISE on one device: every K panel of a row in one pass over its
     CSR (no per-panel re-launch); bit-identical at K = 8, 40 (odd panel

@@ -40,17 +40,30 @@ def standin(request, gpu):
     return request.param, A, X, Yseq, absY, smfv.DeviceCSR(A, gpu), torch.from_numpy(X).to(gpu)
 
 
+# (r5) ROWWISE under the three row partitions: blocks of equal work (the
+# default), the reference's equal rows, and equal-work blocks cut into 3
+# chunks (SMFV_DIST_CHUNKS: one tiled plan per chunk)
+PARTS = [(smfv.Variant.ROWWISE, "balanced", 1), (smfv.Variant.ROWWISE, "reference", 1),
+         (smfv.Variant.ROWWISE, "balanced", 3), (smfv.Variant.COLUMNWISE, "balanced", 1),
+         (smfv.Variant.NONZERO, "balanced", 1)]
+
+
 @pytest.mark.parametrize("p", [2, 4, 8])
-@pytest.mark.parametrize("variant", [smfv.Variant.ROWWISE, smfv.Variant.COLUMNWISE, smfv.Variant.NONZERO])
-def test_rank_plans_full_size(gpu, standin, p, variant):
+@pytest.mark.parametrize("variant,partition,chunks", PARTS)
+def test_rank_plans_full_size(gpu, standin, p, variant, partition, chunks):
     name, A, X, Yseq, absY, dA, dX = standin
     m = A.numRows
     root = p - 1
-    first, last, off, cnt = D.exchange_plan(variant, m, A.nnz, A.rowPtr, K, p)
+    dopts = D.dist_opts(partition, chunks)
+    first, last, off, cnt = D.exchange_plan(variant, m, A.nnz, A.rowPtr, K, p, dopts)
     Y = torch.full((m, K), float("nan"), dtype=torch.float64, device=gpu)
     blocks = []
     for r in range(p):
-        P = D.DistPlan(None, variant, dA, K, to_all=False, root=root, rank=(r, p))
+        P = D.DistPlan(None, variant, dA, K, to_all=False, root=root, rank=(r, p), partition=partition,
+                       chunks=chunks)
+        pf, pl, _, _ = P.partition()  # the plan's own partition is the host function's
+        assert np.array_equal(pf, first) and np.array_equal(pl, last)
+        assert P.shape() == (p, r, chunks)
         P.run_local(dX, Y)
         blocks.append(P.exchange_buffer())
         st = P.stats()

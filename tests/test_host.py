@@ -569,3 +569,41 @@ def test_column_streamed_plan_layout():
     ci = np.array([0, 2, 1, 1, 0], np.int32)  # row 1 unsorted
     with pytest.raises(RuntimeError, match="column-sorted"):
         _lib.call("smfv_cs_plan_analyse", 0, 2, 3, rp.ctypes.data_as(ip), ci.ctypes.data_as(ip), 0, 0, out)
+
+
+def test_balanced_row_partition():
+    """(r5) Distributed ROWWISE plans cut the rows into blocks of equal work
+    (12 B per non-zero + 8K + 4 B per row) unless SMFV_DIST_REFERENCE_ROWS
+    asks for the reference's equal row counts (SC/...RowWise.cpp:26-29,
+    = smfv_dist_plan).  Blocks tile [0, m) in rank order; on a skewed
+    pattern the balanced blocks' work is within one row of the mean, and
+    chunk boundaries tile each block."""
+    from sparsematrixmultiplicationmpi_amd import dist as D
+    A = smfv.gen_random_rows(20000, 20000, 16.0, 2.0, 2000, 77)
+    rp = A.rowPtr.astype(np.int64)
+    K = 32
+    m = A.numRows
+    work = lambda s, e: 12 * (rp[e] - rp[s]) + (8 * K + 4) * (e - s)  # noqa: E731
+    maxrow = int(12 * np.diff(rp).max() + 8 * K + 4)
+    for p in (2, 3, 8, 13):
+        ref = exchange_plan(1, m, A.nnz, A.rowPtr, K, p)
+        assert all(np.array_equal(a, b) for a, b in zip(ref, D.exchange_plan(1, m, A.nnz, A.rowPtr, K, p,
+                                                                             D.REFERENCE_ROWS)))
+        first, last, off, cnt = D.exchange_plan(1, m, A.nnz, A.rowPtr, K, p, D.dist_opts("balanced"))
+        assert first[0] == 0 and last[-1] == m - 1 and np.all(first[1:] == last[:-1] + 1)
+        assert np.all(off == first.astype(np.int64) * K) and np.all(cnt == (last - first + 1).astype(np.int64) * K)
+        wb = [work(int(first[r]), int(last[r]) + 1) for r in range(p)]
+        wr = [work(int(ref[0][r]), int(ref[1][r]) + 1) for r in range(p)]
+        mean = work(0, m) / p
+        assert max(wb) - mean <= maxrow, (p, max(wb) / mean)
+        assert max(wb) <= max(wr), p
+        for chunks in (2, 5):
+            dopts = D.dist_opts("balanced", chunks)
+            for r in range(p):
+                b = D.chunk_rows(1, dopts, m, A.nnz, A.rowPtr, K, p, r)
+                assert len(b) == chunks + 1 and b[0] == first[r] and b[-1] == last[r] + 1 and b == sorted(b)
+    # the power-law pattern is imbalanced under equal rows
+    p = 8
+    ref = exchange_plan(1, m, A.nnz, A.rowPtr, K, p)
+    wr = [work(int(ref[0][r]), int(ref[1][r]) + 1) for r in range(p)]
+    assert max(wr) / (work(0, m) / p) > 1.02
