@@ -1103,10 +1103,10 @@ def main() -> None:
                     help="report the post-timing result check but do not fail on it (lab ablations)")
     ap.add_argument("--mfma", action="store_true",
                     help="time the opt-in dense-block MFMA tile kernel (SMFV_PLAN_MFMA, config 3's MFMA K-panel)")
-    ap.add_argument("--tiled-kernel", default="auto", choices=["auto", "cs", "ws", "ws1", "ws2", "ws3"],
-                    help="tiled kernel for K % 32 == 0: the library's choice, k_rows_cs (SMFV_PLAN_CS) "
-                         "or k_rows_ws (SMFV_PLAN_WS), A/B; ws1 / ws2: k_rows_ws with one 1024-lane / two 512-lane "
-                         "pipelines per CU (SMFV_PLAN_WS_GEOM1 / GEOM2)")
+    ap.add_argument("--tiled-kernel", default="auto", choices=["auto", "ws", "ws1", "ws2", "ws3"],
+                    help="tiled kernel for K % 32 == 0: the library's choice or k_rows_ws (SMFV_PLAN_WS), A/B; "
+                         "ws1 / ws2 / ws3: k_rows_ws with one 1024-lane / two 512-lane / one 768-lane pipeline(s) "
+                         "per CU (SMFV_PLAN_WS_GEOM1 / 2 / 3)")
     ap.add_argument("--fma", action="store_true",
                     help="time the opt-in FMA plans (SMFV_PLAN_FMA) instead of the bit-exact ones")
     ap.add_argument("--rank-plans", type=int, default=0,

@@ -181,14 +181,12 @@ typedef struct smfv_plan_s *smfv_plan_t;
  * variants are checked against (SC/main.cpp:184) -- so that check does not
  * compare a kernel with itself.  Ignored for SMFV_NONZERO. */
 #define SMFV_PLAN_SIMPLE_ROWS 128
-/* LAB BUILD ONLY (libsmfv_lab.so; since r4 libsmfv.so ignores the flag and
- * keeps k_rows_ws): column-streamed tiles (k_rows_cs, K % 32 == 0), two
- * tiles of ~m / 512 rows per CU, each row's 32 panel columns held in
- * registers, the tile's X rows streamed through LDS in column-sorted chunks;
- * bit-identical, measured 3.4x slower than k_rows_ws. */
+/* RETIRED (ignored): column-streamed tiles (k_rows_cs), measured 3.4x slower
+ * than k_rows_ws (profiles/r03/ab_s2/); the r2-r4 lab build that kept it was
+ * removed in r5.  The value stays reserved. */
 #define SMFV_PLAN_CS 256
-/* The former tiled kernel (k_rows_ws: ~60-row tiles whose whole X union sits
- * in LDS) where SMFV_PLAN_CS would be the default (A/B). */
+/* The tiled kernel k_rows_ws (~60-row tiles whose whole X union sits in
+ * LDS), asked for explicitly (with a geometry flag below: A/B). */
 #define SMFV_PLAN_WS 512
 /* (r4) The geometry of k_rows_ws (A/B; without either flag the library's
  * default): GEOM1 one 1024-lane block per CU (8 compute + 8 loader waves,
@@ -254,7 +252,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
  * rows per XCD, 1: one wavefront), [12] X rows the 8 parts read, summed,
  * over the pattern's X rows (-1: not computed), [13] the kernel a tiled
  * plan runs: 0 none (untiled), 1 k_rows_ws, 2 k_rows_mfma, 3 k_spmv_chunks,
- * 4 k_rows_cs (lab); [14] chunks of a k_rows_cs plan; [15] (r4) the k_rows_ws
+ * (4 was the retired k_rows_cs); [14] 0 (reserved); [15] (r4) the k_rows_ws
  * geometry (1: one 1024-lane block per CU, 2: two 512-lane blocks, 3: one
  * 768-lane block; 0 other); [16] (r4) 1 if a bind writes the snapshot's real
  * entries from bind items of up to 4 consecutive non-zeros (pads written once

@@ -1,12 +1,16 @@
 #!/bin/bash
-# A/B: NEW (libsmfv.so) vs OLD (libsmfv_lab.so = a copy of the previous product build), alternating
+# A/B of two builds of the same sources, alternating on one box:
+#   NEW = libsmfv.so (this tree), OLD = libsmfv_ab.so (a copy of the build to
+#   compare against, placed in the package directory before the gpurun call;
+#   loaded with SMFV_LIB=libsmfv_ab.so).  CFGS / ROUNDS / EXTRA select what runs.
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
-mkdir -p gpurun_out
-for cfg in cop20k_k32 cop20k_k128 cop20kirr_k32; do
- for r in 1 2; do
-  for lab in 0 1; do
-    SMFV_LAB=$lab timeout -k 10 200 python bench.py --config $cfg --no-cpu-baseline --no-vendor --no-copy-floor > gpurun_out/ab_${cfg}_${lab}_$r.log 2>&1 || exit $?
-    tail -n 1 gpurun_out/ab_${cfg}_${lab}_$r.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$cfg', 'old' if $lab else 'new', d['ms_per_step']*1e3, d['roofline']['frac'], d['check']['ok'], d['check']['max_abs_diff'])"
+mkdir -p gpurun_out/ab
+for cfg in ${CFGS:-cop20k_k32 cop20k_k128 cop20kirr_k32}; do
+ for r in $(seq 1 ${ROUNDS:-2}); do
+  for lib in libsmfv.so libsmfv_ab.so; do
+    SMFV_LIB=$lib timeout -k 10 200 python bench.py --config $cfg --no-cpu-baseline --no-vendor --no-copy-floor \
+        --no-rebind ${EXTRA:-} > gpurun_out/ab/ab_${cfg}_${lib%.so}_$r.json 2> gpurun_out/ab/ab_${cfg}_${lib%.so}_$r.log || exit $?
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print('$cfg', '$lib', round(d['ms_per_step']*1e3, 3), d['roofline']['frac'], d['check']['ok'], d['check'].get('max_abs_diff'))" gpurun_out/ab/ab_${cfg}_${lib%.so}_$r.json
   done
  done
 done

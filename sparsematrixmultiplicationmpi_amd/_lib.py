@@ -11,9 +11,10 @@ import os
 from ctypes import POINTER, c_char, c_char_p, c_double, c_int, c_int64, c_size_t, c_uint64, c_void_p
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# SMFV_LAB=1 loads the lab build (make -C csrc lab: ablation kernels and
-# environment overrides for A/B experiments); the product is libsmfv.so
-LIB_PATH = os.path.join(HERE, "libsmfv_lab.so" if os.environ.get("SMFV_LAB") == "1" else "libsmfv.so")
+# The product is libsmfv.so.  SMFV_LIB=<file name in this directory> loads
+# another build of the same sources instead -- for A/B runs only, e.g. a copy
+# of the previous build (scripts/ab_lib.sh); the driver never sets it.
+LIB_PATH = os.path.join(HERE, os.path.basename(os.environ.get("SMFV_LIB") or "libsmfv.so"))
 
 SMFV_OK = 0
 STATUS_NAMES = {
@@ -143,14 +144,6 @@ _SIGS = {
 }
 
 
-# lab build only (libsmfv_lab.so): the column-streamed tile plan's analysis
-# (csrc/lab/cs_plan_lab.h), out of the product since r4
-_LAB_SIGS = {
-    "smfv_cs_plan_analyse": (c_int, [c_int, c_int, c_int, _PI, _PI, c_int, c_int, _PD]),
-}
-LAB = LIB_PATH.endswith("libsmfv_lab.so")
-
-
 def _load() -> ctypes.CDLL:
     # torch bundles its own ROCm runtime (libamdhip64.so.7, librccl.so.1,
     # libhsa-runtime64.so.1).  Importing it FIRST makes libsmfv.so's NEEDED
@@ -163,9 +156,7 @@ def _load() -> ctypes.CDLL:
             f"{LIB_PATH} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
             "(make -C sparsematrixmultiplicationmpi_amd/csrc). There is no CPU fallback.")
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
-    for name, (res, args) in (dict(_SIGS, **_LAB_SIGS) if LAB else _SIGS).items():
-        if name in _LAB_SIGS and not hasattr(lib, name):
-            continue  # a product build staged as the lab library (A/B runs)
+    for name, (res, args) in _SIGS.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -45,9 +45,6 @@
 
 #include "smfv_internal.h"
 #include "smfv_plan.h"
-#ifdef SMFV_LAB
-#include "lab/cs_plan_lab.h"  // k_rows_cs plan (lab only)
-#endif
 
 #pragma clang fp contract(off)
 
@@ -275,15 +272,9 @@ __global__ __launch_bounds__(NT) void k_spmv_stream(int row_begin, int nrows, co
 typedef double chunk_d2 __attribute__((ext_vector_type(2)));
 constexpr int K1_NT = 256;  // lanes per chunk block = row cap of a chunk
 
-// entry slots per chunk (1,024; lab builds: SMFV_K1_CHUNK = 512 / 1,024 / 2,048)
+// entry slots per chunk (1,024; 512 and 2,048 measured slower: DESIGN.md 4.1)
 static int spmv_chunk_cap()
 {
-#ifdef SMFV_LAB
-    if (const char *e = std::getenv("SMFV_K1_CHUNK")) {
-        const int v = std::atoi(e);
-        return v == 2048 || v == 512 ? v : 1024;
-    }
-#endif
     return 1024;
 }
 
@@ -353,9 +344,6 @@ __global__ __launch_bounds__(NT) void k_spmv_chunks(const int4 *__restrict__ hdr
     }
 }
 
-#ifdef SMFV_LAB
-#include "lab/spmv_lab.inc"  // k_spmv_pipe (lab A/B, measured slower: DESIGN.md section 7)
-#endif
 
 // ---------------------------------------------------------------------------
 // k_rows_mh: the production row kernel for K even and 16-byte aligned X/Y.
@@ -879,9 +867,6 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
     }
 }
 
-#ifdef SMFV_LAB
-#include "lab/ws_lab.inc"  // the instrumented lab copy (libsmfv_lab.so only)
-#endif
 
 // the product instances of k_rows_ws: geometry (smfv_plan.h WsGeom) x FMA x SADDR x NARROW
 #define SMFV_WS_INST(G_) k_rows_ws<G_.cw, G_.lw, G_.ppw, G_.ucap, G_.ncap, FMA, SADDR, NARROW>
@@ -907,9 +892,6 @@ static auto pick_ws(int geom, bool fma, bool saddr, bool narrow = false)
     return narrow ? pick_ws_n<true>(geom, fma, saddr) : pick_ws_n<false>(geom, fma, saddr);
 }
 
-#ifdef SMFV_LAB
-#include "lab/cs_lab.inc"  // k_rows_cs, column-streamed tiles (lab only since r4: measured 3.4x slower)
-#endif
 
 // Rows the ws plan could not tile (over a cap alone): one 8-lane team per
 // row, X gathered straight from HBM, CSR order (bit-identical).  `rows` are
@@ -1446,22 +1428,13 @@ static int pick_team(int K, int vec)
     }
 
 // Row-kernel configuration (TEAM lanes per row, H column groups per lane,
-// U gathers in flight per team) by K; in the lab build (-DSMFV_LAB)
-// SMFV_ROW_CFG="TEAM,H,U" overrides it for A/B measurement (only
-// configurations instantiated below exist).
+// U gathers in flight per team) by K.
 struct RowCfg {
     int team, h, u;
 };
 
 static RowCfg row_cfg_for(int K)
 {
-#ifdef SMFV_LAB
-    static const char *env = std::getenv("SMFV_ROW_CFG");
-    if (env) {
-        RowCfg c{0, 0, 0};
-        if (std::sscanf(env, "%d,%d,%d", &c.team, &c.h, &c.u) == 3) return c;
-    }
-#endif
     const int pairs = K / 2;  // double2 columns
     if (pairs >= 64) return {16, 4, 4};
     if (pairs >= 16) return {8, 2, 8};
@@ -1520,19 +1493,6 @@ static int launch_rows(int row_begin, int nrows, const int *rp, const int *ci, c
         constexpr int NT = 256, RPB = 64, CH = 2048;
         const int64_t nblk = ((int64_t)nrows + RPB - 1) / RPB;
         SMFV_REQUIRE(nblk <= 0x7fffffff, "too many rows for one launch");
-#ifdef SMFV_LAB
-        static const int pipe_bpc = [] {  // lab A/B: SMFV_K1_PIPE=<blocks per CU> runs k_spmv_pipe
-            const char *e = std::getenv("SMFV_K1_PIPE");
-            return e ? std::atoi(e) : 0;
-        }();
-        if (pipe_bpc > 0) {
-            const int64_t pb = std::min<int64_t>(nblk, (int64_t)256 * pipe_bpc);
-            hipLaunchKernelGGL((k_spmv_pipe<NT, RPB, CH>), dim3((unsigned)pb), dim3(NT), 0, st, row_begin, nrows,
-                               (int)nblk, rp, ci, va, X, ldx, Y, ldy);
-            SMFV_LAUNCHED();
-            return SMFV_OK;
-        }
-#endif
         hipLaunchKernelGGL((k_spmv_stream<NT, RPB, CH>), dim3((unsigned)nblk), dim3(NT), 0, st, row_begin, nrows,
                            rp, ci, va, X, ldx, Y, ldy);
         SMFV_LAUNCHED();
@@ -1602,14 +1562,7 @@ static int launch_merge(int row_first, int nrows, int64_t s, int64_t e, const in
     const int tpb = 256 / team;
     const int64_t nblk = (g.nteams + tpb - 1) / tpb;
     SMFV_REQUIRE(nblk <= 0x7fffffff, "too many merge teams for one launch");
-#ifdef SMFV_LAB
-    static const bool flat = [] {  // lab A/B: SMFV_MERGE_FLAT=0 keeps the per-row k_merge
-        const char *ev = std::getenv("SMFV_MERGE_FLAT");
-        return !ev || std::atoi(ev) != 0;
-    }();
-#else
     constexpr bool flat = true;
-#endif
     if (flat && vec == 2 && K % 32 == 0) {
         const int64_t fblk_ = (g.nteams + 15) / 16;
         hipLaunchKernelGGL((k_merge_flat<16>), dim3((unsigned)fblk_), dim3(256), 0, st, row_first, nrows, s, e, rp,
@@ -1779,11 +1732,6 @@ static TileCaps plan_caps(int flags, int col_base)
     caps.frontier = !(flags & SMFV_PLAN_NATURAL_SEEDS);
     caps.split_ends = (flags & SMFV_PLAN_SPLIT_ENDS) ? SMFV_WS_BLOCKS_PER_XCD : 0;
     caps.col_base = col_base;  // a row block's neighbours are its columns shifted by its first global row
-#ifdef SMFV_LAB
-    // lab: smaller tiles (rows / entries / union) to measure what a unit costs
-    if (const char *e = std::getenv("SMFV_WS_MAXROWS")) caps.maxrows = std::max(8, std::min(caps.maxrows, atoi(e)));
-    if (const char *e = std::getenv("SMFV_WS_UCAP")) caps.ucap = std::max(8, std::min(caps.ucap, atoi(e)));
-#endif
     return caps;
 }
 
@@ -1844,8 +1792,6 @@ struct smfv_plan_s {
     uint16_t *k1_rs = nullptr, *k1_off = nullptr;
     int *k1_col = nullptr;                 // wide layout: 32-bit columns (k1_off unused)
     bool k1_wide = false;
-    bool cs = false;                       // k_rows_cs (column-streamed tiles), ntiles = tiles
-    int cs_chunks = 0;
     int cs_xcd[9] = {};                    // XCD x runs tiles [cs_xcd[x], cs_xcd[x + 1])
     int *cs_bs = nullptr;                  // per block of the 8 x 32 grid: first chunk, chunks per panel
     int *cs_trow = nullptr, *cs_tlast = nullptr, *cs_crec = nullptr;
@@ -2053,51 +1999,7 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                 }
             }
         }
-#ifdef SMFV_LAB
-        // (lab only since r4)
-        // column-streamed tiles (k_rows_cs) where asked for; a pattern the
-        // layout does not take (unsorted rows, ...) keeps k_rows_ws
-        if (!rc && go && !(flags & SMFV_PLAN_MFMA) && (flags & SMFV_PLAN_CS) && !(flags & SMFV_PLAN_WS) &&
-            K % TILE_KP == 0) {
-            CsPlan C;
-            std::string err;
-            if (build_cs_plan(m, n, rpl.data(), cil, C, &err, caps)) {
-                p->tiled = p->cs = true;
-                p->ntiles = C.ntiles;
-                p->cs_chunks = C.nchunks;
-                for (int x = 0; x <= 8; ++x) p->cs_xcd[x] = C.xcd[x];
-                p->parts = caps.part_start.size() > 2 ? (int)caps.part_start.size() - 1 : 1;
-                p->union_rows = C.union_rows;
-                p->tiled_nnz = C.tiled_nnz;
-                p->padded_nnz = C.entries;
-                p->reuse = C.union_rows ? (double)C.tiled_nnz / (double)C.union_rows : 0.0;
-                // per block of the 8 x 32 grid: its first chunk and its chunks (one panel)
-                std::vector<int> bs(2 * 8 * CS_BLOCKS_PER_XCD, 0);
-                for (int blk = 0; blk < 8 * CS_BLOCKS_PER_XCD; ++blk) {
-                    const int x = blk & 7, t0 = C.xcd[x] + (blk >> 3);
-                    if (t0 >= C.xcd[x + 1]) continue;
-                    bs[2 * blk] = C.tfirst[(size_t)t0];
-                    for (int t = t0; t < C.xcd[x + 1]; t += CS_BLOCKS_PER_XCD)
-                        bs[2 * blk + 1] += (t + 1 < C.ntiles ? C.tfirst[(size_t)t + 1] : C.nchunks) - C.tfirst[(size_t)t];
-                }
-                for (int &q : C.tsrc)
-                    if (q >= 0) q += (int)nnz_base;
-                p->snapshot = (int64_t)C.tsrc.size();
-                if (!rc) rc = upload(&p->cs_bs, bs, p->dev_bytes);
-                if (!rc) rc = upload(&p->cs_trow, C.trow, p->dev_bytes);
-                if (!rc) rc = upload(&p->cs_tlast, C.tlast, p->dev_bytes);
-                if (!rc) rc = upload(&p->cs_crec, C.crec, p->dev_bytes);
-                if (!rc) rc = upload(&p->cs_aux, C.aux, p->dev_bytes);
-                if (!rc) rc = upload(&p->tsrc, C.tsrc, p->dev_bytes);
-                if (!rc) {
-                    const size_t b = std::max<size_t>((size_t)p->snapshot, 1) * sizeof(double);
-                    fail_hip(hipMalloc(reinterpret_cast<void **>(&p->tvals), b), "hipMalloc(tvals)");
-                    p->dev_bytes += b;
-                }
-            }
-        }
-#endif
-        if (!rc && go && !p->mfma && !p->cs && !(flags & SMFV_PLAN_MFMA)) {
+        if (!rc && go && !p->mfma && !(flags & SMFV_PLAN_MFMA)) {
             WsPlan W;
             std::string err;
             // a pattern the tile layout cannot take (the replayed plan fails its
@@ -2367,50 +2269,6 @@ SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int
     return SMFV_OK;
 }
 
-#ifdef SMFV_LAB  // lab only since r4 (csrc/lab/cs_plan_lab.h)
-SMFV_API int smfv_cs_plan_analyse(int row_begin, int row_end, int n, const int *h_row_ptr_all,
-                                  const int *h_col_idx_all, int flags, int rows_per_tile, double out[8])
-{
-    SMFV_REQUIRE(row_begin >= 0 && row_end >= row_begin && n >= 0 && h_row_ptr_all && out &&
-                     (h_row_ptr_all[row_end] == h_row_ptr_all[row_begin] || h_col_idx_all),
-                 "bad argument");
-    SMFV_REQUIRE(rows_per_tile >= 0 && rows_per_tile <= CS_ROWS, "rows per tile must be 0..%d", CS_ROWS);
-    const int m = row_end - row_begin, base = h_row_ptr_all[row_begin];
-    std::vector<int> rpl((size_t)m + 1);
-    for (int i = 0; i <= m; ++i) rpl[i] = h_row_ptr_all[row_begin + i] - base;
-    const int *cil = h_col_idx_all ? h_col_idx_all + base : nullptr;
-    TileCaps caps = plan_caps(flags, row_begin);
-    double footprint = -1.0;
-    plan_parts(caps, flags, m, n, rpl.data(), cil, &footprint);
-    caps.cs_rows = rows_per_tile;
-    CsPlan C;
-    std::string err;
-    if (!build_cs_plan(m, n, rpl.data(), cil, C, &err, caps)) {
-        set_error("%s", err.c_str());
-        return SMFV_ERR_INVALID;
-    }
-    int most = 0, steps = 0;  // chunks / SIMD steps of the busiest block of the 8 x 32 grid
-    for (int blk = 0; blk < 8 * CS_BLOCKS_PER_XCD; ++blk) {
-        const int x = blk & 7;
-        int units = 0, st = 0;
-        for (int t = C.xcd[x] + (blk >> 3); t < C.xcd[x + 1]; t += CS_BLOCKS_PER_XCD) {
-            units += (t + 1 < C.ntiles ? C.tfirst[(size_t)t + 1] : C.nchunks) - C.tfirst[(size_t)t];
-            st += C.tsimd[(size_t)t];
-        }
-        most = std::max(most, units);
-        steps = std::max(steps, st);
-    }
-    out[0] = C.ntiles;
-    out[1] = C.nchunks;
-    out[2] = (double)C.union_rows;
-    out[3] = C.union_rows ? (double)C.tiled_nnz / (double)C.union_rows : 0.0;
-    out[4] = (double)C.entries;
-    out[5] = (double)C.tiled_nnz;
-    out[6] = most;
-    out[7] = steps;
-    return SMFV_OK;
-}
-#endif
 
 SMFV_API int smfv_spmv_chunks_analyse(int row_begin, int row_end, int n, const int *h_row_ptr_all,
                                       const int *h_col_idx_all, int cap, double out[6])
@@ -2508,9 +2366,9 @@ SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS])
     out[10] = plan->mfma ? 1.0 : 0.0;
     out[11] = plan->parts;
     out[12] = plan->footprint;
-    out[13] = !plan->tiled ? 0.0 : plan->cs ? 4.0 : plan->k1 ? 3.0 : plan->mfma ? 2.0 : 1.0;
-    out[14] = plan->cs_chunks;
-    out[15] = plan->tiled && !plan->cs && !plan->k1 && !plan->mfma ? plan->ws_geom : 0;
+    out[13] = !plan->tiled ? 0.0 : plan->k1 ? 3.0 : plan->mfma ? 2.0 : 1.0;
+    out[14] = 0.0;  // (r5: k_rows_cs retired with the lab build)
+    out[15] = plan->tiled && !plan->k1 && !plan->mfma ? plan->ws_geom : 0;
     out[16] = plan->bind_desc ? 1.0 : 0.0;
     return SMFV_OK;
 }
@@ -2575,12 +2433,6 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
     if (plan->k1) {
         if (plan->ntiles > 0) {
             auto kern = plan->k1_wide ? k_spmv_chunks<K1_NT, 1024, true> : k_spmv_chunks<K1_NT, 1024, false>;
-#ifdef SMFV_LAB
-            if (plan->k1_cap == 2048)
-                kern = plan->k1_wide ? k_spmv_chunks<K1_NT, 2048, true> : k_spmv_chunks<K1_NT, 2048, false>;
-            if (plan->k1_cap == 512)
-                kern = plan->k1_wide ? k_spmv_chunks<K1_NT, 512, true> : k_spmv_chunks<K1_NT, 512, false>;
-#endif
             hipLaunchKernelGGL(kern, dim3((unsigned)plan->ntiles), dim3(K1_NT), 0, st,
                                reinterpret_cast<const int4 *>(plan->k1_hdr), plan->k1_rs, plan->k1_off, plan->k1_col,
                                plan->tvals, d_X, ldx, d_Y, ldy);
@@ -2593,24 +2445,6 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         int v = 0;
         if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
     }
-#ifdef SMFV_LAB  // k_rows_cs: lab only since r4
-    if (plan->cs) {
-        // 8 x 32 persistent blocks (the plan's per-block chunk lists assume
-        // that grid; on a chip with fewer CUs blocks queue, still correct);
-        // the loaders address X, the snapshot and the aux bytes by scalar
-        // base + 32-bit offset
-        if ((uint64_t)plan->n * (uint64_t)ldx * 8u >= (1ull << 32))
-            return launch_rows(plan->row_begin, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, plan->n, K, d_Y, ldy,
-                               st);
-        CsXcd xr;
-        for (int x = 0; x <= 8; ++x) xr.first[x] = plan->cs_xcd[x];
-        hipLaunchKernelGGL(plan->fma ? k_rows_cs<true> : k_rows_cs<false>, dim3(8 * CS_BLOCKS_PER_XCD), dim3(1024),
-                           0, st, xr, K / TILE_KP, reinterpret_cast<const int2 *>(plan->cs_bs), plan->cs_trow,
-                           plan->cs_tlast, plan->cs_crec, plan->cs_aux, plan->tvals, d_X, ldx, d_Y, ldy);
-        SMFV_LAUNCHED();
-        return SMFV_OK;
-    }
-#endif
     if (plan->mfma) {
         if (plan->ntiles > 0) {
             hipLaunchKernelGGL(k_rows_mfma, dim3((unsigned)plan->ntiles), dim3(256), 0, st, K / TILE_KP, plan->mf_rec,
@@ -2627,42 +2461,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         // snapshot each span < 4 GiB
         const bool saddr = (uint64_t)plan->n * (uint64_t)ldx * 8u < (1ull << 32) &&
                            (uint64_t)plan->snapshot * 8u < (1ull << 32);
-#ifdef SMFV_LAB
-        static const int abl = [] {  // lab-only ablations (k_rows_ws ABL modes)
-            const char *e = std::getenv("SMFV_WS_ABL");
-            return e ? std::atoi(e) : 0;
-        }();
-        static const bool lab_saddr = [] {  // lab A/B: SMFV_WS_SADDR=0 keeps 64-bit per-lane addresses
-            const char *e = std::getenv("SMFV_WS_SADDR");
-            return !e || std::atoi(e) != 0;
-        }();
-        static const int lab_chunked = [] {  // lab A/B: SMFV_WS_CHUNKED=0/1 overrides the tile order
-            const char *e = std::getenv("SMFV_WS_CHUNKED");
-            return e ? std::atoi(e) : -1;
-        }();
-        if (lab_chunked >= 0) chunked = lab_chunked;
-        auto kern = plan->fma ? (abl == 2 ? k_rows_ws_lab<2, true> : WS1<true, true>)
-                  : abl == 1 ? k_rows_ws_lab<1> : abl == 2 ? k_rows_ws_lab<2> : abl == 3 ? k_rows_ws_lab<3>
-                  : abl == 4 ? k_rows_ws_lab<4> : abl == 5 ? k_rows_ws_lab<5> : abl == 6 ? k_rows_ws_lab<6>
-                  : abl == 7 ? k_rows_ws_lab<7> : abl == 8 ? k_rows_ws_lab<8> : abl == 12 ? k_rows_ws_lab<12>
-                  : abl == 13 ? k_rows_ws_lab<13> : abl == 14 ? k_rows_ws_lab<14> : abl == 15 ? k_rows_ws_lab<15> : abl == 16 ? k_rows_ws_lab<16>
-                  : abl == 9 ? (K == TILE_KP ? k_rows_ws_lab<9> : WS1<false, true>)
-                  : abl == 10 ? (K == TILE_KP ? k_rows_ws_lab<10> : WS1<false, true>)
-                  : abl == 11 ? (K == TILE_KP ? k_rows_ws_lab<11> : WS1<false, true>)
-                  : abl == 17 ? (K == TILE_KP && plan->m >= 120000 ? k_rows_ws_lab<17> : WS1<false, true>) : WS1<false, true>;
-        // the lab's ablation copies are geometry 1 only
-        if (!(saddr && lab_saddr) || plan->ws_geom != 1) kern = pick_ws(plan->ws_geom, plan->fma, saddr && lab_saddr);
-        static unsigned long long *stamp_buf = nullptr;
-        const size_t stamp_n = (size_t)blocks * 16 * WS_STAMP_UNITS * 2;
-        if (abl == 8 && !stamp_buf) {
-            SMFV_HIP(hipMalloc(reinterpret_cast<void **>(&stamp_buf), 256 * 16 * WS_STAMP_UNITS * 2 * 8));
-            SMFV_HIP(hipMemcpyToSymbol(HIP_SYMBOL(ws_stamps), &stamp_buf, sizeof(stamp_buf)));
-        }
-        SMFV_REQUIRE(abl != 8 || blocks <= 256, "lab stamps: at most 256 blocks");
-        if (abl == 8) SMFV_HIP(hipMemsetAsync(stamp_buf, 0, stamp_n * 8, st));
-#else
         auto kern = pick_ws(plan->ws_geom, plan->fma, saddr);
-#endif
         WsXcd xr;
         for (int x = 0; x <= 8; ++x) xr.first[x] = plan->ws_xcd[x];
         const int threads = ws_geom(plan->ws_geom).threads();
@@ -2675,18 +2474,6 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3((unsigned)threads), 0, st, xr,
                            narrow ? 1 : K / TILE_KP, chunked, plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();
-#ifdef SMFV_LAB
-        if (abl == 8)
-            if (const char *path = std::getenv("SMFV_WS_STAMPS")) {  // eager runs only: dump this launch's stamps
-                std::vector<unsigned long long> h(stamp_n);
-                SMFV_HIP(hipStreamSynchronize(st));
-                SMFV_HIP(hipMemcpy(h.data(), stamp_buf, stamp_n * 8, hipMemcpyDeviceToHost));
-                if (FILE *f = std::fopen(path, "wb")) {
-                    std::fwrite(h.data(), 8, h.size(), f);
-                    std::fclose(f);
-                }
-            }
-#endif
     }
     if (plan->ndirect > 0) {
         hipLaunchKernelGGL(k_rows_list, dim3((unsigned)((plan->ndirect + 31) / 32), (unsigned)std::max(1, K / TILE_KP)),

@@ -122,7 +122,6 @@ struct TileCaps {
     std::vector<int> part_rows, part_start;
     int xcd_blocks = 32;           // k_rows_ws blocks per XCD (MI355X: 256 CUs / 8 XCDs)
     WsGeom geom = WS_GEOM1;        // build_ws_plan: the kernel geometry (ucap / ncap / maxrows follow it)
-    int cs_rows = 0;               // build_cs_plan: rows per tile (0: the fewest rounds of <= CS_ROWS per block)
 };
 // Independent parts are analysed on up to 8 threads; analysis_threads > 0
 // caps that for analyses run on the calling thread (smfv_set_analysis_threads).

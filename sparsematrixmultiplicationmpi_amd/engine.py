@@ -119,7 +119,7 @@ PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA, PLAN_NATURAL_SEEDS, PLAN_MFMA, PLAN_S
 PLAN_ONE_WAVEFRONT, PLAN_SIMPLE_ROWS, PLAN_CS, PLAN_WS = 64, 128, 256, 512
 PLAN_WS_GEOM1, PLAN_WS_GEOM2, PLAN_WS_GEOM3 = 1024, 2048, 4096
 PLAN_STATS = 17  # SMFV_PLAN_STATS
-PLAN_KERNELS = {0: None, 1: "k_rows_ws", 2: "k_rows_mfma", 3: "k_spmv_chunks", 4: "k_rows_cs"}
+PLAN_KERNELS = {0: None, 1: "k_rows_ws", 2: "k_rows_mfma", 3: "k_spmv_chunks"}
 
 
 class SpmmPlan:
@@ -154,11 +154,11 @@ class SpmmPlan:
             flags |= PLAN_SPLIT_ENDS
         if {"auto": False, "one": True}[xcd_parts]:
             flags |= PLAN_ONE_WAVEFRONT
-        # which tiled kernel for K % 32 == 0: the library's choice, or k_rows_cs
-        # (column-streamed tiles, SMFV_PLAN_CS) / k_rows_ws (SMFV_PLAN_WS) for
-        # A/B; "ws1" / "ws2": k_rows_ws with one 1024-lane / two 512-lane
-        # pipelines per CU (SMFV_PLAN_WS_GEOM1 / GEOM2)
-        flags |= {"auto": 0, "cs": PLAN_CS, "ws": PLAN_WS, "ws1": PLAN_WS | PLAN_WS_GEOM1,
+        # which tiled kernel for K % 32 == 0: the library's choice, or k_rows_ws
+        # (SMFV_PLAN_WS) for A/B; "ws1" / "ws2" / "ws3": k_rows_ws with one
+        # 1024-lane / two 512-lane / one 768-lane pipeline(s) per CU
+        # (SMFV_PLAN_WS_GEOM1 / 2 / 3)
+        flags |= {"auto": 0, "ws": PLAN_WS, "ws1": PLAN_WS | PLAN_WS_GEOM1,
                   "ws2": PLAN_WS | PLAN_WS_GEOM2, "ws3": PLAN_WS | PLAN_WS_GEOM3}[tiled_kernel]
         self._plan = ctypes.c_void_p()
         ip = ctypes.POINTER(ctypes.c_int)

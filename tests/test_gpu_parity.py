@@ -878,66 +878,3 @@ def test_mfma_tile_kernel_within_tolerance(gpu, K):
         plan.run(torch.from_numpy(X).to(gpu), Y)
         torch.cuda.synchronize()
         assert np.all(np.abs(Y.cpu().numpy() - Yref) <= 1e-12 * scale + 1e-300)
-
-
-def test_column_streamed_flag_ignored_by_the_product(gpu):
-    """(r4) k_rows_cs is lab-only: in libsmfv.so SMFV_PLAN_CS is ignored and
-    the plan runs k_rows_ws, bit-identical to the reference order."""
-    if smfv._lib.LAB:
-        pytest.skip("the lab build keeps k_rows_cs")
-    A = smfv.gen_fem27(6000, 20, 20, 0.83, 3)
-    X = np.random.default_rng(3).uniform(-1, 1, (A.numCols, 32))
-    plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(A, gpu), 32, tiles="force", tiled_kernel="cs")
-    assert plan.stats()["kernel"] == "k_rows_ws"
-    Y = torch.full((A.numRows, 32), np.nan, dtype=torch.float64, device=gpu)
-    plan.run(torch.from_numpy(X).to(gpu), Y)
-    torch.cuda.synchronize()
-    assert np.array_equal(bits(Y.cpu().numpy()), bits(oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)))
-
-
-@pytest.mark.skipif(not smfv._lib.LAB, reason="lab build only (SMFV_LAB=1 loads libsmfv_lab.so)")
-@pytest.mark.parametrize("K", [32, 64])
-def test_column_streamed_tiles_opt_in(gpu, K):
-    """Opt-in SMFV_PLAN_CS (k_rows_cs, measured slower than k_rows_ws and not
-    the default): tiles of ~m/512 rows with each row's panel columns held in
-    registers while the tile's column-sorted X rows stream through LDS in
-    chunks; a row's entries are consumed chunk by chunk in CSR order, so the
-    result is bit-identical to the reference loop.  Tiny patterns (one chunk,
-    empty rows, a duplicate entry), every row length 0..40 in a local window,
-    and the full cop20k_A stand-in (several chunks per tile, K = 64: two
-    panels re-stream the chunks)."""
-    import os
-    from sparsematrixmultiplicationmpi_amd import inputs
-    rng = np.random.default_rng(11 + K)
-    m = n = 3000
-    lens = np.arange(m) % 41
-    rp = np.zeros(m + 1, np.int32)
-    rp[1:] = np.cumsum(lens)
-    ci = np.concatenate([np.sort(rng.choice(np.arange(max(0, i - 60), min(n, i + 60)), L, replace=False))
-                         for i, L in enumerate(lens)]).astype(np.int32)
-    mats = [smfv.readMatrixMarketFile(os.path.join(os.path.dirname(__file__), "golden", f))
-            for f in ("sym5.mtx", "pat4x6.mtx", "empty7x5.mtx")]
-    mats.append(smfv.SparseMatrix(values=rng.uniform(-1, 1, ci.size), colIndices=ci, rowPtr=rp, numRows=m,
-                                  numCols=n))
-    for A in mats:
-        X = rng.uniform(-1, 1, (A.numCols, K))
-        Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
-        plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(A, gpu), K, tiles="force", tiled_kernel="cs")
-        assert plan.stats()["kernel"] == "k_rows_cs"
-        Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
-        plan.run(torch.from_numpy(X).to(gpu), Y)
-        torch.cuda.synchronize()
-        assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref))
-    A = inputs.cop20k_surrogate()
-    dA = smfv.DeviceCSR(A, gpu)
-    X = torch.from_numpy(rng.uniform(-1, 1, (A.numCols, K))).to(gpu)
-    ref = smfv.SpmmPlan(smfv.Variant.SEQUENTIAL, dA, K, tiles="off")
-    plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiled_kernel="cs")
-    st = plan.stats()
-    assert st["kernel"] == "k_rows_cs" and st["chunks"] > st["tiles"]
-    Yr = torch.empty((A.numRows, K), dtype=torch.float64, device=gpu)
-    Y = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
-    ref.run(X, Yr)
-    plan.run(X, Y)
-    torch.cuda.synchronize()
-    assert torch.equal(Y.view(torch.int64), Yr.view(torch.int64))

@@ -539,36 +539,18 @@ def test_spmv_chunk_layout():
     assert np.diff(P.rowPtr).max() > 2048 and not _chunks(P, cap=2048)["fits"]
 
 
-def test_column_streamed_plan_is_lab_only():
-    """(r4) The column-streamed tile kernel (k_rows_cs, measured 3.4x slower)
-    lives in the lab build only: libsmfv.so exports no k_rows_cs symbol and no
-    smfv_cs_plan_analyse; libsmfv_lab.so keeps both for A/B."""
+def test_no_lab_code_in_the_product():
+    """(r5) The r2-r4 lab build (ablation copies of the kernels, environment
+    overrides, k_rows_cs) is retired: no source of the product mentions it
+    and libsmfv.so exports no k_rows_cs / smfv_cs_plan_analyse.  A/B runs
+    load another build of the same sources (SMFV_LIB), never an ifdef path."""
     nm = subprocess.run(["nm", "-D", "-C", os.path.join(PKG, "libsmfv.so")], capture_output=True, text=True).stdout
     assert "smfv_cs_plan_analyse" not in nm and "k_rows_cs" not in nm
-    lab = os.path.join(PKG, "libsmfv_lab.so")
-    if os.path.exists(lab):
-        nm = subprocess.run(["nm", "-D", lab], capture_output=True, text=True).stdout
-        assert "smfv_cs_plan_analyse" in nm
-
-
-@pytest.mark.skipif(not _lib.LAB, reason="lab build only (SMFV_LAB=1 loads libsmfv_lab.so)")
-def test_column_streamed_plan_layout():
-    """The opt-in column-streamed tile plan (k_rows_cs, SMFV_PLAN_CS), built and
-    verified natively (every row's entries replayed chunk by chunk in CSR
-    order, pads on the zero image row): on the cop20k stand-in about two tiles
-    per CU, several chunks per tile, more X re-use than the k_rows_ws tiles;
-    a row whose columns are not sorted is refused (the plan keeps k_rows_ws)."""
-    A = smfv.inputs.cop20k_surrogate()
-    ip = ctypes.POINTER(ctypes.c_int)
-    out = (ctypes.c_double * 8)()
-    _lib.call("smfv_cs_plan_analyse", 0, A.numRows, A.numCols, A.rowPtr.ctypes.data_as(ip),
-              A.colIndices.ctypes.data_as(ip), 0, 0, out)
-    tiles, chunks, reuse, nnz = int(out[0]), int(out[1]), out[3], int(out[5])
-    assert 256 < tiles <= 512 and chunks > 2 * tiles and reuse > 6.0 and nnz == A.nnz
-    rp = np.array([0, 3, 5], np.int32)
-    ci = np.array([0, 2, 1, 1, 0], np.int32)  # row 1 unsorted
-    with pytest.raises(RuntimeError, match="column-sorted"):
-        _lib.call("smfv_cs_plan_analyse", 0, 2, 3, rp.ctypes.data_as(ip), ci.ctypes.data_as(ip), 0, 0, out)
+    csrc = os.path.join(PKG, "csrc")
+    assert not os.path.exists(os.path.join(csrc, "lab"))
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".cpp", ".h", ".inc")):
+            assert "SMFV_LAB" not in open(os.path.join(csrc, f)).read(), f
 
 
 def test_balanced_row_partition():
