@@ -670,18 +670,18 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     ncopies = max(1, min(16, math.ceil(args.cold_bytes / prob_bytes) + 1))
     V = smfv.Variant[variant]
     rows = V in (smfv.Variant.ROWWISE, smfv.Variant.SEQUENTIAL)
-    # the plans timed per copy: the value's step first (the default plan:
-    # work-balanced row blocks, all-gather to every rank), then beside it the
-    # reference's exchange semantics (blocks to rank 0 only, MPI_Gatherv /
-    # MPI_Reduce, SC/...RowWise.cpp:85-87), the reference's equal-row
-    # partition (SC/...RowWise.cpp:26-29) and the chunked exchange
+    # the plans timed per copy: the value's step first (the default plan: the
+    # reference's equal-row blocks, SC/...RowWise.cpp:26-29, all-gathered to
+    # every rank), then beside it the reference's exchange semantics (blocks
+    # to rank 0 only, MPI_Gatherv / MPI_Reduce, SC/...RowWise.cpp:85-87), the
+    # other row partition (SMFV_DIST_BALANCED_ROWS) and the chunked exchange
     # (SMFV_DIST_CHUNKS: chunk j's all-gatherv overlapped with chunk j + 1's
     # compute)
     kinds = {"value": dict(to_all=True, partition=args.partition)}
     kinds["gather_to_root"] = dict(to_all=False, partition=args.partition)
     if rows:
-        kinds["reference_rows"] = dict(to_all=True, partition="reference" if args.partition == "balanced"
-                                       else "balanced")
+        other = "reference" if args.partition == "balanced" else "balanced"
+        kinds[f"{other}_rows"] = dict(to_all=True, partition=other)
         if args.chunks > 1:
             kinds[f"chunked{args.chunks}"] = dict(to_all=True, partition=args.partition, chunks=args.chunks)
     copies, t_plan = [], 0.0
@@ -798,7 +798,7 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
             "exchange_note": "exchange_ms: all-gather of Y to every rank (the value's step); "
                              "plans_beside.gather_to_root: the reference's semantics, blocks gathered to rank 0 "
                              "only (MPI_Gatherv, SC/...RowWise.cpp:85-87 / MPI_Reduce, ...NonZeroElement.cpp:88); "
-                             "reference_rows: the reference's equal-row partition; chunkedC: C row chunks per "
+                             "balanced_rows / reference_rows: the other row partition; chunkedC: C row chunks per "
                              "rank, each chunk's point-to-point all-gatherv started as soon as it is computed; "
                              "each exchange_ms = (kernel + exchange) - kernel alone, max over ranks",
             "timing": how,
@@ -853,7 +853,7 @@ def bench_rank_plans(args, kind: str, K: int, variant: str) -> None:
     ncopies = max(1, min(16, math.ceil(args.cold_bytes / prob_bytes) + 1))
     rowwise = V == smfv.Variant.ROWWISE
     chunks = args.rank_chunks if rowwise else 1
-    part = args.partition if rowwise else "balanced"
+    part = args.partition if rowwise else "reference"
     copies = []
     for c in range(ncopies):
         dA = smfv.DeviceCSR(A, dev)
@@ -1113,9 +1113,9 @@ def main() -> None:
                     help="p > 0: a one-GPU projection of the p-rank decomposition -- every rank's share timed in "
                          "turn through its rank plan (smfv_dist_plan_create_rank); prints a projection line, not "
                          "the headline")
-    ap.add_argument("--partition", default="balanced", choices=["balanced", "reference"],
-                    help="decomposed / --rank-plans ROWWISE: row blocks of equal work (default) or the reference's "
-                         "equal row counts (SC/...RowWise.cpp:26-29)")
+    ap.add_argument("--partition", default="reference", choices=["balanced", "reference"],
+                    help="decomposed / --rank-plans ROWWISE: the reference's equal row counts (SC/...RowWise.cpp:26-29, "
+                         "default) or row blocks of equal work (SMFV_DIST_BALANCED_ROWS)")
     ap.add_argument("--chunks", type=int, default=2,
                     help="decomposed ROWWISE: also time the chunked exchange with this many row chunks per rank "
                          "(SMFV_DIST_CHUNKS; 1 = skip)")

@@ -368,15 +368,18 @@ SMFV_API int smfv_dist_plan(int variant, int m, int64_t nnz, const int *h_row_pt
 
 /* (r5) Distribution options: the high byte of a distributed plan's flags
  * (the low bits stay smfv_plan_create's SMFV_PLAN_* flags for the rank's
- * share), and the `dopts` of the *_opts host functions below.
- *   SMFV_DIST_REFERENCE_ROWS  ROWWISE row blocks by the reference's formula,
- *        equal row counts (SC/...RowWise.cpp:26-29).  Without it a
- *        distributed ROWWISE plan cuts the rows into blocks of equal WORK:
- *        12 B per non-zero + 8K + 4 B per row (the block's CSR and Y bytes),
- *        so an irregular pattern's ranks finish together.  The result is
- *        bit-identical either way: each row is summed in CSR order by the one
- *        rank that owns it.  The Gatherv / all-gatherv exchange takes any
- *        block sizes (SC/...RowWise.cpp:85-87 does too).
+ * share), and the `dopts` of the *_opts host functions below.  0 = the
+ * reference's decomposition.
+ *   SMFV_DIST_BALANCED_ROWS  ROWWISE row blocks of equal WORK, 12 B per
+ *        non-zero + 8K + 4 B per row (the block's CSR and Y bytes), instead
+ *        of the reference's equal row counts (SC/...RowWise.cpp:26-29).  The
+ *        result is bit-identical either way: each row is summed in CSR order
+ *        by the one rank that owns it, and the Gatherv / all-gatherv exchange
+ *        takes any block sizes.  Opt-in: measured on the irregular cop20k_A
+ *        stand-in at p = 8 it cuts the slowest rank's kernel 12.1 -> 11.5 us
+ *        but makes the Y blocks unequal (the largest 3.9 -> 5.6 MB), so the
+ *        exchange, which dominates the step, loses the single ncclAllGather
+ *        and moves more bytes per link.
  *   SMFV_DIST_CHUNKS(c)  ROWWISE, c = 2..7: the rank's block is cut into c
  *        row chunks of equal work, each a row-block plan of its own; chunk
  *        j's exchange is issued on the plan's exchange stream as soon as
@@ -386,13 +389,13 @@ SMFV_API int smfv_dist_plan(int variant, int m, int64_t nnz, const int *h_row_pt
  *        of theirs (TO_ALL, an all-gatherv over the full xGMI mesh) or to the
  *        root (TO_ROOT, the Gatherv).  0 / 1: one block, one exchange.
  * Row-partitioned plans (A not replicated) always use the reference rows. */
-#define SMFV_DIST_REFERENCE_ROWS (1 << 24)
+#define SMFV_DIST_BALANCED_ROWS (1 << 24)
 #define SMFV_DIST_CHUNKS(c) (((c) & 7) << 25)
 #define SMFV_DIST_CHUNKS_OF(f) (((f) >> 25) & 7)
 #define SMFV_DIST_OPTS (0xFF << 24)
 /* smfv_dist_plan under distribution options (h_row_ptr needed for
  * work-balanced ROWWISE blocks; NULL falls back to the reference rows).
- * smfv_dist_plan(...) = smfv_dist_plan_opts(..., SMFV_DIST_REFERENCE_ROWS). */
+ * smfv_dist_plan(...) = smfv_dist_plan_opts(..., 0). */
 SMFV_API int smfv_dist_plan_opts(int variant, int dopts, int m, int64_t nnz, const int *h_row_ptr, int K, int p,
                                  int *first, int *last, int64_t *offset, int64_t *count);
 /* ROWWISE under SMFV_DIST_CHUNKS(c): rank `rank`'s chunk boundaries,

@@ -213,7 +213,7 @@ SMFV_API int smfv_dist_plan_opts(int variant, int dopts, int m, int64_t nnz, con
                                  int *first, int *last, int64_t *offset, int64_t *count)
 {
     const bool rows = variant == SMFV_ROWWISE || variant == SMFV_SEQUENTIAL;
-    if (!rows || (dopts & SMFV_DIST_REFERENCE_ROWS) || !h_row_ptr)
+    if (!rows || !(dopts & SMFV_DIST_BALANCED_ROWS) || !h_row_ptr)
         return smfv_dist_plan(variant, m, nnz, h_row_ptr, K, p, first, last, offset, count);
     SMFV_REQUIRE(m >= 0 && K >= 0 && p > 0, "bad argument");
     SMFV_REQUIRE(first && last && offset && count, "null output array");
@@ -237,10 +237,9 @@ struct Plan {
     int chunks = 1;         // (r5) ROWWISE: row chunks per rank, each exchanged on its own
     std::vector<int> cb;    // chunked: rank r's chunk j = rows [cb[r (chunks + 1) + j], cb[r (chunks + 1) + j + 1])
 };
-// (the plain host functions and the plan-less smfv_dist_spmm_f64 keep the
+// (the plain host functions and the plan-less smfv_dist_spmm_f64 take the
 // reference's partition; distributed plans pass their own options)
-int make_plan(int variant, int m, int64_t nnz, const int *h_row_ptr, int K, int p, Plan &P,
-              int dopts = SMFV_DIST_REFERENCE_ROWS)
+int make_plan(int variant, int m, int64_t nnz, const int *h_row_ptr, int K, int p, Plan &P, int dopts = 0)
 {
     P.first.assign(p, 0);
     P.last.assign(p, -1);

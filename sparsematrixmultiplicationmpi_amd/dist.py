@@ -26,17 +26,17 @@ UNIQUE_ID_BYTES = 128
 TO_ROOT, TO_ALL = 0, 1
 # (r5) distribution options (include/smfv.h SMFV_DIST_*), the high byte of a
 # distributed plan's flags
-REFERENCE_ROWS = 1 << 24
+BALANCED_ROWS = 1 << 24
 
 
-def dist_opts(partition: str = "balanced", chunks: int = 1) -> int:
-    """SMFV_DIST_* bits: ROWWISE row blocks of equal work ("balanced", the
-    distributed plans' default) or the reference's equal row counts
-    ("reference", SC/...RowWise.cpp:26-29); `chunks` row chunks per rank,
-    each exchanged as soon as it is computed (SMFV_DIST_CHUNKS)."""
+def dist_opts(partition: str = "reference", chunks: int = 1) -> int:
+    """SMFV_DIST_* bits: ROWWISE row blocks by the reference's equal row
+    counts ("reference", SC/...RowWise.cpp:26-29, the default) or of equal
+    work ("balanced", SMFV_DIST_BALANCED_ROWS); `chunks` row chunks per
+    rank, each exchanged as soon as it is computed (SMFV_DIST_CHUNKS)."""
     if partition not in ("balanced", "reference") or not 1 <= chunks <= 7:
         raise ValueError(f"partition {partition!r}, chunks {chunks}")
-    return (REFERENCE_ROWS if partition == "reference" else 0) | ((chunks & 7) << 25 if chunks > 1 else 0)
+    return (BALANCED_ROWS if partition == "balanced" else 0) | ((chunks & 7) << 25 if chunks > 1 else 0)
 
 
 def _rp(row_ptr):
@@ -47,7 +47,7 @@ def _rp(row_ptr):
 
 
 def exchange_plan(variant: int, m: int, nnz: int, row_ptr: np.ndarray | None, K: int, p: int,
-                  dopts: int = REFERENCE_ROWS):
+                  dopts: int = 0):
     """Native smfv_dist_plan_opts: per-rank (first, last, offset, count)
     arrays; by default the reference's partition (smfv_dist_plan)."""
     first = np.zeros(p, dtype=np.int32)
@@ -127,7 +127,7 @@ EX_ALLGATHER, EX_BCAST, EX_SEND, EX_RECV = 1, 2, 3, 4  # SMFV_EX_*
 
 
 def exchange_ops(variant: int, mode: int, root: int, m: int, nnz: int, row_ptr: np.ndarray | None, K: int,
-                 p: int, rank: int, dopts: int = REFERENCE_ROWS, chunk: int = 0) -> list[tuple[int, int, int, int]]:
+                 p: int, rank: int, dopts: int = 0, chunk: int = 0) -> list[tuple[int, int, int, int]]:
     """Native smfv_dist_exchange_ops_opts: the exchange step of `rank` (of
     chunk `chunk` under SMFV_DIST_CHUNKS) as a list of (kind, peer, offset,
     count) -- the schedule the RCCL path runs, in one group."""
@@ -173,7 +173,7 @@ class DistPlan:
     def __init__(self, comm: Communicator | None, variant: int, A: DeviceCSR, K: int, to_all: bool,
                  root: int = 0, tiles: str = "auto", rowpart: bool = False, m: int | None = None,
                  stream=None, rank: tuple[int, int] | None = None, fma: bool = False, tiled_kernel: str = "auto",
-                 partition: str = "balanced", chunks: int = 1):
+                 partition: str = "reference", chunks: int = 1):
         self.comm, self.variant, self.A, self.K = comm, Variant(variant), A, K
         self.mode = TO_ALL if to_all else TO_ROOT
         self.root = root
@@ -183,8 +183,9 @@ class DistPlan:
         # the rank share's tiled-kernel geometry (SpmmPlan's tiled_kernel; A/B)
         flags |= {"auto": 0, "ws1": PLAN_WS | PLAN_WS_GEOM1, "ws2": PLAN_WS | PLAN_WS_GEOM2,
                   "ws3": PLAN_WS | PLAN_WS_GEOM3}[tiled_kernel]
-        # (r5) ROWWISE blocks of equal work by default ("reference": equal rows);
-        # chunks > 1: per-chunk exchanges overlapped with the next chunk's compute
+        # (r5) ROWWISE: the reference's equal rows by default, "balanced": blocks
+        # of equal work; chunks > 1: per-chunk exchanges overlapped with the
+        # next chunk's compute
         flags |= dist_opts(partition, chunks)
         ip = POINTER(c_int)
         self._h = c_void_p()

@@ -554,9 +554,9 @@ def test_no_lab_code_in_the_product():
 
 
 def test_balanced_row_partition():
-    """(r5) Distributed ROWWISE plans cut the rows into blocks of equal work
-    (12 B per non-zero + 8K + 4 B per row) unless SMFV_DIST_REFERENCE_ROWS
-    asks for the reference's equal row counts (SC/...RowWise.cpp:26-29,
+    """(r5) SMFV_DIST_BALANCED_ROWS cuts a distributed ROWWISE plan's rows
+    into blocks of equal work (12 B per non-zero + 8K + 4 B per row); without
+    it the blocks are the reference's equal row counts (SC/...RowWise.cpp:26-29,
     = smfv_dist_plan).  Blocks tile [0, m) in rank order; on a skewed
     pattern the balanced blocks' work is within one row of the mean, and
     chunk boundaries tile each block."""
@@ -570,7 +570,7 @@ def test_balanced_row_partition():
     for p in (2, 3, 8, 13):
         ref = exchange_plan(1, m, A.nnz, A.rowPtr, K, p)
         assert all(np.array_equal(a, b) for a, b in zip(ref, D.exchange_plan(1, m, A.nnz, A.rowPtr, K, p,
-                                                                             D.REFERENCE_ROWS)))
+                                                                             D.dist_opts("reference"))))
         first, last, off, cnt = D.exchange_plan(1, m, A.nnz, A.rowPtr, K, p, D.dist_opts("balanced"))
         assert first[0] == 0 and last[-1] == m - 1 and np.all(first[1:] == last[:-1] + 1)
         assert np.all(off == first.astype(np.int64) * K) and np.all(cnt == (last - first + 1).astype(np.int64) * K)
