@@ -200,6 +200,12 @@ typedef struct smfv_plan_s *smfv_plan_t;
  * pieces each), 64-row tiles: 3 waves per SIMD, so the compute waves may hold
  * up to 168 VGPRs (deeper LDS read-ahead). */
 #define SMFV_PLAN_WS_GEOM3 4096
+/* (r5) Live values: the tiled kernel's loaders DMA each row's value pairs
+ * straight from the caller's CSR values (no snapshot, no bind pass: a bind is
+ * a no-op and every execute reads the values it is given, like an untiled
+ * plan).  Bit-identical to the snapshot path.  Tiled k_rows_ws plans only
+ * (K = 1 chunk plans and SMFV_PLAN_MFMA keep their snapshot). */
+#define SMFV_PLAN_LIVE_VALUES 8192
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
 /* Plan of the row block [row_begin, row_end) of a CSR matrix (h_row_ptr /
@@ -252,7 +258,8 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
  * rows per XCD, 1: one wavefront), [12] X rows the 8 parts read, summed,
  * over the pattern's X rows (-1: not computed), [13] the kernel a tiled
  * plan runs: 0 none (untiled), 1 k_rows_ws, 2 k_rows_mfma, 3 k_spmv_chunks,
- * (4 was the retired k_rows_cs); [14] 0 (reserved); [15] (r4) the k_rows_ws
+ * (4 was the retired k_rows_cs); [14] (r5) 1 if the tiled plan reads live
+ * values (SMFV_PLAN_LIVE_VALUES), else 0; [15] (r4) the k_rows_ws
  * geometry (1: one 1024-lane block per CU, 2: two 512-lane blocks, 3: one
  * 768-lane block; 0 other); [16] (r4) 1 if a bind writes the snapshot's real
  * entries from bind items of up to 4 consecutive non-zeros (pads written once

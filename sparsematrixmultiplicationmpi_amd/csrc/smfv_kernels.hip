@@ -553,6 +553,28 @@ template <bool NT> __device__ __forceinline__ void dma16s(const void *base, unsi
                      : "=&s"(keep) : "v"(voff), "s"(sb), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
 }
 __device__ __forceinline__ void barrier_lds() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// (r5) The same through a buffer descriptor (SGPR quad) + 32-bit per-lane byte
+// offset, non-temporal: the range check returns 0 for every dword at or past
+// the descriptor's num_records (measured per dword on MI355X:
+// scripts/micro/lds_dma_probe.hip), so a 16-byte piece that straddles the end
+// of the caller's array reads no byte past it.  voff need only be 8-byte
+// aligned (LDS-DMA of 8-byte aligned 16-byte pieces: exact, same probe).
+typedef int bufrsrc __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void dma16b(bufrsrc r, unsigned voff, unsigned lds_dst)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen nt lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(voff), "s"(r), "s"(__builtin_amdgcn_readfirstlane(lds_dst)) : "memory");
+}
+// a raw buffer over [base, base + bytes) (bytes < 4 GiB), wave-uniform
+__device__ __forceinline__ bufrsrc make_rsrc(const void *base, unsigned bytes)
+{
+    const uint64_t b = (uint64_t)(uintptr_t)base;
+    return bufrsrc{__builtin_amdgcn_readfirstlane((int)(uint32_t)b),
+                   __builtin_amdgcn_readfirstlane((int)((b >> 32) & 0xFFFF)),
+                   __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000};
+}
 
 // (r4) LDS layout of a k_rows_ws geometry (WsGeom, smfv_plan.h): two X
 // images of UCAP + 1 rows (the last one zero), then two meta slots of values,
@@ -580,14 +602,20 @@ template <int CW, int LW, int PPW, int UCAP, int NCAP> struct Lay {
 struct WsXcd {
     int first[9];  // XCD x runs tiles [first[x], first[x + 1]) of the plan's order
 };
-template <int CW, int LW, int PPW, int UCAP, int NCAP, bool FMA = false, bool SADDR = true, bool NARROW = false>
+// (r5) LIVE: the loaders DMA the value pairs straight from the caller's CSR
+// values (tv = the block's first value, tv_bytes its bytes) at the CSR index
+// vidx[t * vstride + slot] of each slot (WsPlan::live): no snapshot, no bind
+template <int CW, int LW, int PPW, int UCAP, int NCAP, bool FMA = false, bool SADDR = true, bool NARROW = false,
+          bool LIVE = false>
 __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsXcd xr, int npanel, int chunked,
                                                      const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
                                                      const uint8_t *__restrict__ loff,
                                                      const double *__restrict__ tv,
                                                      const double *__restrict__ X, int64_t ldx,
-                                                     double *__restrict__ Y, int64_t ldy)
+                                                     double *__restrict__ Y, int64_t ldy,
+                                                     const int *__restrict__ vidx = nullptr, int vstride = 0,
+                                                     unsigned tv_bytes = 0)
 {
     using namespace ws;
     using L = Lay<CW, LW, PPW, UCAP, NCAP>;
@@ -641,6 +669,12 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
         int noff, tn, nu, voff, tnv;
         unsigned xo[PPW];                     // SADDR: byte offset of this lane's 16 B of union row uc[i]
         const unsigned ldxb = (unsigned)(ldx * 8);
+        // LIVE: this lane's value slot in each of the wave's value pieces
+        // (pieces wl, wl + LW, ...: VI at most), as byte offsets into tv
+        constexpr int VI = (NCAP + 128 * LW - 1) / (128 * LW);
+        unsigned vo[LIVE ? VI : 1] = {};
+        bufrsrc vr{};
+        if constexpr (LIVE) vr = make_rsrc(tv, tv_bytes);
         auto fetch_record = [&](int t) {
             const int *G = grec + (int64_t)t * WS_GWORDS;
             const i4 *gu = reinterpret_cast<const i4 *>(G + 4 * PPW * wl + PPW * (lane >> 4));
@@ -651,6 +685,14 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
             nu = G[WS_G_NU + (lane & 15)];
             voff = G[WS_G_VOFF + (lane & 15)];
             tnv = G[WS_G_TNV + (lane & 15)];
+            if constexpr (LIVE) {
+                // the slots' CSR indices load beside the record, a unit before
+                // their DMAs (no dependent round trip in front of the stage)
+                const int *vt = vidx + (int64_t)t * vstride + 64 * wl + lane;
+#pragma unroll
+                for (int i = 0; i < VI; ++i)
+                    if (64 * (wl + LW * i) < vstride) vo[i] = 8u * (unsigned)vt[64 * LW * i];
+            }
         };
         // stage unit (tile t, panel p): X rows into X slot xs, and (first panel) the meta into slot ms
         auto stage = [&](int t, int p, int xs, int ms) {
@@ -659,6 +701,10 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
 #pragma unroll
             for (int k = 0; k < PPW / 4; ++k) asm volatile("" ::"v"(ur[k]));
             asm volatile("" ::"v"(noff), "v"(tn), "v"(nu), "v"(voff), "v"(tnv));
+            if constexpr (LIVE)
+                if (p == 0)
+#pragma unroll
+                    for (int i = 0; i < VI; ++i) asm volatile("" ::"v"(vo[i]));
             const unsigned xb = lds0 + xs * XSLOT;
             int uc[PPW];
 #pragma unroll
@@ -671,7 +717,18 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
                     for (int i = 0; i < PPW; ++i) xo[i] = (unsigned)uc[i] * ldxb + 16u * (unsigned)(lane & XLANE);
             auto stage_meta = [&]() {
                 const unsigned mb = lds0 + SL_M + ms * MSLOT;
-                if constexpr (SADDR) {
+                if constexpr (LIVE) {  // value pairs from the CSR values (SADDR for the rest)
+#pragma unroll
+                    for (int i = 0; i < VI; ++i) {
+                        const int k = wl + LW * i;
+                        if (k * 128 < tnv) dma16b(vr, vo[i], mb + M_V + k * 1024);
+                    }
+                    const uint8_t *lb = loff + __builtin_amdgcn_readfirstlane(noff);
+                    for (int k = wl; k * 1024 < tn; k += LW)
+                        dma16s<true>(lb, 1024u * k + 16u * lane, mb + M_L + k * 1024);
+                    if (wl == LW - 1 && lane < L::REC_LANES)
+                        dma16s<true>(lrec + (int64_t)t * WS_LWORDS, 16u * lane, mb + M_R);
+                } else if constexpr (SADDR) {
                     const int nf = __builtin_amdgcn_readfirstlane(noff);
                     const double *tvb = tv + __builtin_amdgcn_readfirstlane(voff);
                     const uint8_t *lb = loff + nf;
@@ -750,7 +807,17 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
             const int js = info & 0xFFFF, len = info >> 16, nbat = len >> 3, rem = len & 7;
             const int blast = nbat + (rem ? 1 : 0) - 1;
             const u2 *Lq = reinterpret_cast<const u2 *>(mbase + M_L) + js + qk;
-            const d2 *Vq = reinterpret_cast<const d2 *>(mbase + M_V) + R[2 * L::R + slot] + qk;
+            const int vw = R[2 * L::R + slot];
+            const d2 *Vq = reinterpret_cast<const d2 *>(mbase + M_V) + (vw & 0xFFFF) + qk;
+            if constexpr (LIVE)
+                if (vw & (1 << 30)) {
+                    // a row of odd length: its last pair's second half is the
+                    // CSR value after the row (another row's, or 0 past the
+                    // block); -0.0 there before the sums read it (in order:
+                    // one wave's LDS operations execute in program order)
+                    const unsigned a = (unsigned)(uintptr_t)(Vq + 4 * ((len >> 1) - 1)) + 8u;
+                    asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(-0.0) : "memory");
+                }
             const char *xb0 = xbase + par * 128 + tl * 16;
             const char *xb1 = xbase + (par ^ 1) * 128 + tl * 16;
             d2 acc0 = {0.0, 0.0}, acc1 = {0.0, 0.0};
@@ -869,27 +936,29 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsX
 
 
 // the product instances of k_rows_ws: geometry (smfv_plan.h WsGeom) x FMA x SADDR x NARROW
-#define SMFV_WS_INST(G_) k_rows_ws<G_.cw, G_.lw, G_.ppw, G_.ucap, G_.ncap, FMA, SADDR, NARROW>
-template <bool FMA, bool SADDR, bool NARROW = false> constexpr auto WS1 = SMFV_WS_INST(WS_GEOM1);
-template <bool FMA, bool SADDR, bool NARROW = false> constexpr auto WS2 = SMFV_WS_INST(WS_GEOM2);
-template <bool FMA, bool SADDR, bool NARROW = false> constexpr auto WS3 = SMFV_WS_INST(WS_GEOM3);
+#define SMFV_WS_INST(G_) k_rows_ws<G_.cw, G_.lw, G_.ppw, G_.ucap, G_.ncap, FMA, SADDR, NARROW, LIVE>
+template <bool FMA, bool SADDR, bool NARROW, bool LIVE> constexpr auto WS1 = SMFV_WS_INST(WS_GEOM1);
+template <bool FMA, bool SADDR, bool NARROW, bool LIVE> constexpr auto WS2 = SMFV_WS_INST(WS_GEOM2);
+template <bool FMA, bool SADDR, bool NARROW, bool LIVE> constexpr auto WS3 = SMFV_WS_INST(WS_GEOM3);
 #undef SMFV_WS_INST
-template <bool NARROW>
+template <bool NARROW, bool LIVE>
 static auto pick_ws_n(int geom, bool fma, bool saddr)
 {
     if (geom == 2)
-        return fma ? (saddr ? WS2<true, true, NARROW> : WS2<true, false, NARROW>)
-                   : (saddr ? WS2<false, true, NARROW> : WS2<false, false, NARROW>);
+        return fma ? (saddr ? WS2<true, true, NARROW, LIVE> : WS2<true, false, NARROW, LIVE>)
+                   : (saddr ? WS2<false, true, NARROW, LIVE> : WS2<false, false, NARROW, LIVE>);
     if (geom == 3)
-        return fma ? (saddr ? WS3<true, true, NARROW> : WS3<true, false, NARROW>)
-                   : (saddr ? WS3<false, true, NARROW> : WS3<false, false, NARROW>);
-    return fma ? (saddr ? WS1<true, true, NARROW> : WS1<true, false, NARROW>)
-               : (saddr ? WS1<false, true, NARROW> : WS1<false, false, NARROW>);
+        return fma ? (saddr ? WS3<true, true, NARROW, LIVE> : WS3<true, false, NARROW, LIVE>)
+                   : (saddr ? WS3<false, true, NARROW, LIVE> : WS3<false, false, NARROW, LIVE>);
+    return fma ? (saddr ? WS1<true, true, NARROW, LIVE> : WS1<true, false, NARROW, LIVE>)
+               : (saddr ? WS1<false, true, NARROW, LIVE> : WS1<false, false, NARROW, LIVE>);
 }
-// (r4) narrow: a K = 4 / 8 / 16 window (one accumulator per lane)
-static auto pick_ws(int geom, bool fma, bool saddr, bool narrow = false)
+// (r4) narrow: a K = 4 / 8 / 16 window (one accumulator per lane); (r5) live:
+// value pairs DMA'd from the caller's CSR values (LIVE: SADDR always)
+static auto pick_ws(int geom, bool fma, bool saddr, bool narrow = false, bool live = false)
 {
-    return narrow ? pick_ws_n<true>(geom, fma, saddr) : pick_ws_n<false>(geom, fma, saddr);
+    if (live) return narrow ? pick_ws_n<true, true>(geom, fma, true) : pick_ws_n<false, true>(geom, fma, true);
+    return narrow ? pick_ws_n<true, false>(geom, fma, saddr) : pick_ws_n<false, false>(geom, fma, saddr);
 }
 
 
@@ -1779,6 +1848,9 @@ struct smfv_plan_s {
     int *bind_items = nullptr;             // (r4) 2 ints per bind item (k_bind_items)
     int64_t nbind_items = 0;
     bool bind_desc = false;                // bind by k_bind_items (pads filled at creation)
+    bool live = false;                     // (r5) k_rows_ws reads the live CSR values (ws_vidx): no snapshot
+    int *ws_vidx = nullptr;                // live: per tile value slot, its first entry's block-local CSR index
+    int ws_vstride = 0;
     double *tvals = nullptr;               // the bound values snapshot (tile order, pads -0.0, then direct rows)
     const double *bound_values = nullptr;  // d_values the snapshot came from
     int *ws_grec = nullptr, *ws_lrec = nullptr, *direct_rows = nullptr;
@@ -1810,7 +1882,7 @@ struct smfv_plan_s {
     ~smfv_plan_s()
     {
         delete sub;
-        for (void *q : {(void *)tsrc, (void *)bind_items, (void *)tvals, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
+        for (void *q : {(void *)tsrc, (void *)bind_items, (void *)tvals, (void *)ws_vidx, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
                         (void *)direct_off, (void *)ws_loff, ws, (void *)mf_rec, (void *)mf_ucols, (void *)mf_bstep,
                         (void *)k1_hdr, (void *)k1_rs, (void *)k1_off, (void *)k1_col, (void *)cs_bs,
                         (void *)cs_trow, (void *)cs_tlast, (void *)cs_crec, (void *)cs_aux})
@@ -1952,6 +2024,10 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
         const int *cil = h_ci + nnz_base;
         bool go = true;
         TileCaps caps = plan_caps(flags, col_base);
+        // (r5) live values: the tiled kernel DMAs value pairs straight from the
+        // CSR values through a buffer descriptor over the block's values
+        caps.live = (flags & SMFV_PLAN_LIVE_VALUES) && !(flags & SMFV_PLAN_MFMA) && K != 1 &&
+                    p->nnz * 8 < ((int64_t)1 << 32);
         if (!(flags & SMFV_PLAN_FORCE_TILES) && m > SMFV_TILE_SAMPLE_MIN_ROWS) {
             // estimate re-use on the first tiles (frontier-grown in the full
             // pattern, one part) before any O(nnz) pass of the full analysis
@@ -2020,6 +2096,7 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                 }
                 if (2 * W.ntiles < 3 * ncu) {
                     TileCaps c2 = plan_caps(flags | SMFV_PLAN_WS_GEOM2, col_base);
+                    c2.live = caps.live;
                     c2.part_rows = caps.part_rows;
                     c2.part_start = caps.part_start;
                     WsPlan W2;
@@ -2041,7 +2118,21 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                 p->padded_nnz = W.ventries;
                 p->ndirect = (int)W.direct.size();
                 p->reuse = W.union_rows ? (double)W.tiled_nnz / (double)W.union_rows : 0.0;
-                if (p->reuse >= SMFV_TILE_MIN_REUSE || (flags & SMFV_PLAN_FORCE_TILES)) {
+                if ((p->reuse >= SMFV_TILE_MIN_REUSE || (flags & SMFV_PLAN_FORCE_TILES)) && W.live) {
+                    // (r5) live values: no snapshot; direct rows read the CSR
+                    // values too (their offset = their global CSR start)
+                    p->tiled = p->live = true;
+                    p->ws_vstride = W.vstride;
+                    std::vector<int64_t> doff;
+                    doff.reserve(W.direct.size());
+                    for (int r : W.direct) doff.push_back(nnz_base + rpl[r]);
+                    if (!rc) rc = upload(&p->ws_grec, W.grec, p->dev_bytes);
+                    if (!rc) rc = upload(&p->ws_lrec, W.lrec, p->dev_bytes);
+                    if (!rc) rc = upload(&p->ws_loff, W.loff, p->dev_bytes);
+                    if (!rc) rc = upload(&p->ws_vidx, W.vidx, p->dev_bytes);
+                    if (!rc) rc = upload(&p->direct_rows, W.direct, p->dev_bytes);
+                    if (!rc) rc = upload(&p->direct_off, doff, p->dev_bytes);
+                } else if (p->reuse >= SMFV_TILE_MIN_REUSE || (flags & SMFV_PLAN_FORCE_TILES)) {
                     p->tiled = true;
                     // snapshot sources: tile entries (+ DMA slack), then each direct row's values in CSR order
                     std::vector<int> &ts = W.tsrc;
@@ -2301,7 +2392,7 @@ SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, voi
 {
     SMFV_REQUIRE(plan, "null plan");
     if (plan->sub) return smfv_plan_bind_values(plan->sub, d_values, stream);  // (the cut rows read live values)
-    if (!plan->tiled) return SMFV_OK;
+    if (!plan->tiled || plan->live) return SMFV_OK;  // (r5) live plans read the values at execute
     SMFV_REQUIRE(d_values || plan->nnz == 0, "null values");
     hipStream_t st = as_stream(stream);
     const int64_t cnt = plan->snapshot;
@@ -2367,7 +2458,7 @@ SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS])
     out[11] = plan->parts;
     out[12] = plan->footprint;
     out[13] = !plan->tiled ? 0.0 : plan->k1 ? 3.0 : plan->mfma ? 2.0 : 1.0;
-    out[14] = 0.0;  // (r5: k_rows_cs retired with the lab build)
+    out[14] = plan->live ? 1.0 : 0.0;  // (r5) live values (k_rows_cs, which used this slot, is retired)
     out[15] = plan->tiled && !plan->k1 && !plan->mfma ? plan->ws_geom : 0;
     out[16] = plan->bind_desc ? 1.0 : 0.0;
     return SMFV_OK;
@@ -2414,11 +2505,11 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             return launch_rows_simple(plan->row_begin, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, K, d_Y, ldy, st);
         return launch_rows(plan->row_begin, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, plan->n, K, d_Y, ldy, st);
     }
-    if (d_values != plan->bound_values) {
+    if (!plan->live && d_values != plan->bound_values) {
         set_error("tiled plan: values not bound (call smfv_plan_bind_values with these d_values)");
         return SMFV_ERR_INVALID;
     }
-    if (st != plan->bind_stream) {
+    if (!plan->live && st != plan->bind_stream) {
         // the snapshot was gathered on another stream: order this launch after it
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         SMFV_HIP(hipStreamIsCapturing(st, &cs));
@@ -2461,24 +2552,32 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         // snapshot each span < 4 GiB
         const bool saddr = (uint64_t)plan->n * (uint64_t)ldx * 8u < (1ull << 32) &&
                            (uint64_t)plan->snapshot * 8u < (1ull << 32);
-        auto kern = pick_ws(plan->ws_geom, plan->fma, saddr);
+        auto kern = pick_ws(plan->ws_geom, plan->fma, saddr, false, plan->live);
         WsXcd xr;
         for (int x = 0; x <= 8; ++x) xr.first[x] = plan->ws_xcd[x];
         const int threads = ws_geom(plan->ws_geom).threads();
         // (r4) K = 4 / 8 / 16: one panel, a narrow column window (chunked bits 16-23)
         const bool narrow = K < TILE_KP;
         if (narrow) {
-            kern = pick_ws(plan->ws_geom, plan->fma, saddr, true);
+            kern = pick_ws(plan->ws_geom, plan->fma, saddr, true, plan->live);
             chunked = (chunked & 1) | (K << 16);
         }
+        if (plan->live && !saddr) {
+            set_error("live-values tiled plan: X must span < 4 GiB (n * ldx * 8)");
+            return SMFV_ERR_INVALID;
+        }
+        // live: the value pairs come from the block's CSR values through a
+        // range-checked buffer (the last odd row's read past the end gives 0)
+        const double *tv = plan->live ? d_values + plan->nnz_base : plan->tvals;
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3((unsigned)threads), 0, st, xr,
-                           narrow ? 1 : K / TILE_KP, chunked, plan->ws_grec, plan->ws_lrec, plan->ws_loff, plan->tvals, d_X, ldx, d_Y, ldy);
+                           narrow ? 1 : K / TILE_KP, chunked, plan->ws_grec, plan->ws_lrec, plan->ws_loff, tv, d_X, ldx,
+                           d_Y, ldy, plan->ws_vidx, plan->ws_vstride, (unsigned)(plan->nnz * 8));
         SMFV_LAUNCHED();
     }
     if (plan->ndirect > 0) {
         hipLaunchKernelGGL(k_rows_list, dim3((unsigned)((plan->ndirect + 31) / 32), (unsigned)std::max(1, K / TILE_KP)),
                            dim3(256), 0, st, plan->ndirect, K < TILE_KP ? K : 0, plan->direct_rows, plan->direct_off, plan->row_begin,
-                           d_row_ptr, d_col_idx, plan->tvals, d_X, ldx, d_Y, ldy);
+                           d_row_ptr, d_col_idx, plan->live ? d_values : plan->tvals, d_X, ldx, d_Y, ldy);
         SMFV_LAUNCHED();
     }
     return SMFV_OK;

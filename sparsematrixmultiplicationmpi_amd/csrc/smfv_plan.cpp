@@ -361,7 +361,10 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
         if (r < 0 || r >= m || seen[r]) return fail("direct row out of range or repeated");
         seen[r] = 1;
     }
-    if ((int64_t)P.loff.size() != P.entries + WS_SLACK || (int64_t)P.tsrc.size() != P.ventries + WS_SLACK)
+    if ((int64_t)P.loff.size() != P.entries + WS_SLACK ||
+        (P.live ? (P.vstride != G.ncap / 2 || (int64_t)P.vidx.size() != (int64_t)P.ntiles * P.vstride + WS_SLACK ||
+                   !P.tsrc.empty())
+                : (int64_t)P.tsrc.size() != P.ventries + WS_SLACK))
         return fail("entry arrays");
     // headers and row ownership (sequential: every row in exactly one place)
     for (int t = 0; t < P.ntiles; ++t) {
@@ -401,10 +404,17 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
         for (int slot = 0; slot < R; ++slot) {
             const int r = l[slot];
             if (r == -1) continue;
-            const int lb = l[R + slot] & 0xFFFF, len = l[R + slot] >> 16, vb = l[2 * R + slot];
+            const int lb = l[R + slot] & 0xFFFF, len = l[R + slot] >> 16, vb = l[2 * R + slot] & 0xFFFF;
             const int k = (slot / G.cw) & 3;  // the team's position in its quad
             const int rl = rp[r + 1] - rp[r];
             if (len % 2 || len < rl || len > rl + 1) return "row segment length";
+            if ((l[2 * R + slot] & ~0xFFFF) != (P.live && rl % 2 ? 1 << 30 : 0)) return "row value flags";
+            if (P.live)  // each value slot the row sums starts at its pair of CSR values
+                for (int c = 0; c < len / 2; ++c) {
+                    const int64_t s = (int64_t)t * P.vstride + vb + 4 * c + k;
+                    if (vb + 4 * c + k >= P.vstride || 2 * (vb + 4 * c + k) >= tnv) return "value slot leaves its tile";
+                    if (P.vidx[(size_t)s] != rp[r] + 2 * c) return "value slot is not its row's CSR pair";
+                }
             // the entries the kernel sums (len: the row's, rounded up to even);
             // past them its reads only prefetch (never summed), so a quad's
             // last batch may store fewer value pairs than offsets
@@ -423,9 +433,10 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
                         const int j = rp[r] + el;
                         const int u_ = P.loff[le];
                         const int w = (u_ / 4) % G.lw, i = (u_ / 4) / G.lw, qq = u_ % 4;
-                        if (P.tsrc[ve] != j || P.loff[le] == G.ucap || u_ >= nu || g[G.gword(w, qq, i)] != ci[j])
+                        if ((!P.live && P.tsrc[ve] != j) || P.loff[le] == G.ucap || u_ >= nu ||
+                            g[G.gword(w, qq, i)] != ci[j])
                             return "row entry is not its CSR non-zero";
-                    } else if (P.tsrc[ve] != -1 || P.loff[le] != G.ucap) {
+                    } else if ((!P.live && P.tsrc[ve] != -1) || P.loff[le] != G.ucap) {
                         return "pad entry does not read the zero row";
                     }
                 }
@@ -526,6 +537,8 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     P = WsPlan();
     const WsGeom G = caps.geom;
     P.geom = G;
+    P.live = caps.live;
+    P.vstride = caps.live ? G.ncap / 2 : 0;
     if ((G.cw != 8 && G.cw != 4) || G.ucap + 1 > 4 * G.lw * G.ppw || 4 * G.ppw * G.lw > WS_G_NOFF) {
         if (err) *err = "ws plan: unsupported geometry";
         return false;
@@ -610,11 +623,14 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
                     const int el = j - rp[r];
                     P.loff[(size_t)(noff + (int64_t)(lbase + 4 * (el / 8) + k) * 8 + el % 8)] =
                         (uint8_t)pos[ci[j]];
-                    P.tsrc[(size_t)(vnoff + (int64_t)(vbase + 4 * (el / 2) + k) * 2 + el % 2)] = j;
+                    if (!P.live) P.tsrc[(size_t)(vnoff + (int64_t)(vbase + 4 * (el / 2) + k) * 2 + el % 2)] = j;
                 }
+                const int rl = rp[r + 1] - rp[r];
+                if (P.live)  // (r5) value slot of pair c: its first entry's CSR index
+                    for (int c = 0; c < len2(r) / 2; ++c) P.vidx[(size_t)t * P.vstride + vbase + 4 * c + k] = rp[r] + 2 * c;
                 lrec[slot] = r;
                 lrec[NR + slot] = lbase | (len2(r) << 16);
-                lrec[2 * NR + slot] = vbase;
+                lrec[2 * NR + slot] = vbase | (P.live && rl % 2 ? 1 << 30 : 0);
                 tiled += rp[r + 1] - rp[r];
             }
             e += 32 * nb;
@@ -738,7 +754,10 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         return false;
     }
     P.loff.assign((size_t)(P.entries + WS_SLACK), (uint8_t)G.ucap);
-    P.tsrc.assign((size_t)(P.ventries + WS_SLACK), -1);
+    if (P.live)
+        P.vidx.assign((size_t)nt * P.vstride + WS_SLACK, 0);
+    else
+        P.tsrc.assign((size_t)(P.ventries + WS_SLACK), -1);
     P.grec.assign((size_t)nt * WS_GWORDS, 0);
     P.lrec.assign((size_t)nt * WS_LWORDS, 0);
     {

@@ -122,6 +122,7 @@ struct TileCaps {
     std::vector<int> part_rows, part_start;
     int xcd_blocks = 32;           // k_rows_ws blocks per XCD (MI355X: 256 CUs / 8 XCDs)
     WsGeom geom = WS_GEOM1;        // build_ws_plan: the kernel geometry (ucap / ncap / maxrows follow it)
+    bool live = false;             // build_ws_plan: live values (WsPlan::vidx) instead of a snapshot (tsrc)
 };
 // Independent parts are analysed on up to 8 threads; analysis_threads > 0
 // caps that for analyses run on the calling thread (smfv_set_analysis_threads).
@@ -135,7 +136,19 @@ struct WsPlan {
     std::vector<int> grec;         // WS_GWORDS per tile
     std::vector<int> lrec;         // WS_LWORDS per tile
     std::vector<uint8_t> loff;     // per offset entry: its X row in the LDS image (union position; WS_UCAP: pad)
-    std::vector<int> tsrc;         // per value entry: CSR index of its value (-1: pad)
+    std::vector<int> tsrc;         // per value entry: CSR index of its value (-1: pad); empty when live
+    // (r5) live values (TileCaps::live): the kernel's loaders DMA each value
+    // pair straight from the caller's CSR values -- pair c of a row is
+    // values[rp[r] + 2c], values[rp[r] + 2c + 1] (8-byte aligned: LDS-DMA
+    // takes it) -- so no snapshot and no bind pass.  vidx[t * vstride + s]:
+    // the (block-local) CSR index of value slot s's first entry in tile t
+    // (slots no row sums: 0).  A row of odd length L reads one value past
+    // its end (the next row's first, or past the block: the kernel's buffer
+    // descriptor returns 0 there); bit 30 of its V base word flags it, and
+    // its team writes -0.0 over that half in LDS before summing
+    bool live = false;
+    int vstride = 0;               // value slots per tile in vidx (ncap / 2)
+    std::vector<int> vidx;
     std::vector<int> direct;       // rows over a cap alone, gathered straight from X
     int64_t union_rows = 0;        // X rows staged per 32-column panel
     int64_t tiled_nnz = 0;         // non-zeros in tiles (not direct)

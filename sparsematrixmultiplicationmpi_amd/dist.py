@@ -173,13 +173,13 @@ class DistPlan:
     def __init__(self, comm: Communicator | None, variant: int, A: DeviceCSR, K: int, to_all: bool,
                  root: int = 0, tiles: str = "auto", rowpart: bool = False, m: int | None = None,
                  stream=None, rank: tuple[int, int] | None = None, fma: bool = False, tiled_kernel: str = "auto",
-                 partition: str = "reference", chunks: int = 1):
+                 partition: str = "reference", chunks: int = 1, live_values: bool = False):
         self.comm, self.variant, self.A, self.K = comm, Variant(variant), A, K
         self.mode = TO_ALL if to_all else TO_ROOT
         self.root = root
         self.m = A.m if not rowpart else int(m)
-        from .engine import PLAN_WS, PLAN_WS_GEOM1, PLAN_WS_GEOM2, PLAN_WS_GEOM3
-        flags = {"auto": 0, "off": 1, "force": 2}[tiles] | (4 if fma else 0)
+        from .engine import PLAN_LIVE_VALUES, PLAN_WS, PLAN_WS_GEOM1, PLAN_WS_GEOM2, PLAN_WS_GEOM3
+        flags = {"auto": 0, "off": 1, "force": 2}[tiles] | (4 if fma else 0) | (PLAN_LIVE_VALUES if live_values else 0)
         # the rank share's tiled-kernel geometry (SpmmPlan's tiled_kernel; A/B)
         flags |= {"auto": 0, "ws1": PLAN_WS | PLAN_WS_GEOM1, "ws2": PLAN_WS | PLAN_WS_GEOM2,
                   "ws3": PLAN_WS | PLAN_WS_GEOM3}[tiled_kernel]

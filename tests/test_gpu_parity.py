@@ -878,3 +878,115 @@ def test_mfma_tile_kernel_within_tolerance(gpu, K):
         plan.run(torch.from_numpy(X).to(gpu), Y)
         torch.cuda.synchronize()
         assert np.all(np.abs(Y.cpu().numpy() - Yref) <= 1e-12 * scale + 1e-300)
+
+
+# ---------------------------------------------------------------------------
+# (r5) live values (SMFV_PLAN_LIVE_VALUES): the tiled kernel's loaders DMA the
+# value pairs straight from the caller's CSR values -- no snapshot, no bind.
+# Bit-identical to the reference; a row of odd length reads one value past
+# its end (the next row's first, or past the block through a range-checked
+# buffer: 0), which its team overwrites with -0.0 before summing, so even a
+# NaN / inf in the next row stays out of it.
+# ---------------------------------------------------------------------------
+def _live_run(A, X, gpu, K=None, rows=None, live=True, tiles="force", Xd=None):
+    dA = smfv.DeviceCSR(A, gpu)
+    K = X.shape[1] if K is None else K
+    Xd = torch.from_numpy(np.ascontiguousarray(X)).to(gpu) if Xd is None else Xd
+    m = A.numRows if rows is None else rows[1] - rows[0]
+    plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles=tiles, rows=rows, live_values=live)
+    Y = torch.full((m, K), np.nan, dtype=torch.float64, device=gpu)
+    plan.run(Xd, Y)
+    torch.cuda.synchronize()
+    return plan, Y.cpu().numpy()
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_live_values_golden(gpu, name):
+    g = load_golden(name)
+    A = mat(g["row_ptr"], g["col_idx"], g["values"], g["m"], g["n"])
+    K = g["X"].shape[1]
+    plan, Y = _live_run(A, g["X"], gpu)
+    if K % 32 == 0 or K in (4, 8, 16):
+        assert plan.stats()["live_values"] and plan.stats()["snapshot_entries"] == 0
+    assert np.array_equal(bits(Y), bits(g["Y_seq"])), name
+
+
+@pytest.mark.parametrize("K", [4, 8, 16, 32, 64, 128])
+def test_live_values_odd_rows_and_block_end(gpu, K):
+    """Odd row lengths everywhere (1..41), the last row odd with nnz odd (its
+    pair's second half lies past the array: the buffer's range check gives
+    0), NaN and inf as the first value of rows that follow odd rows (never in
+    the odd row's sum), and row blocks starting at odd CSR indices."""
+    rng = np.random.default_rng(100 + K)
+    m = n = 2600
+    lens = (np.arange(m) * 7) % 41 + 1
+    lens[-1] = 13
+    rp = np.zeros(m + 1, np.int64)
+    rp[1:] = np.cumsum(lens)
+    if rp[-1] % 2 == 0:
+        lens[-2] += 1
+        rp[1:] = np.cumsum(lens)
+    assert rp[-1] % 2 == 1
+    ci = np.concatenate([np.sort(rng.choice(np.arange(max(0, i - 50), min(n, i + 50)), L, replace=False))
+                         for i, L in enumerate(lens)]).astype(np.int32)
+    va = rng.uniform(-1, 1, ci.size)
+    bad = [i for i in range(1, m) if lens[i - 1] % 2 == 1][:40:3]
+    va[rp[bad[::2]]] = np.nan
+    va[rp[bad[1::2]]] = np.inf
+    A = mat(rp.astype(np.int32), ci, va, m, n)
+    X = rng.uniform(-1, 1, (n, K))
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+
+    def same(Y, Yr):  # bit for bit where finite; NaN exactly where the reference has NaN
+        nan = np.isnan(Yr)
+        return np.array_equal(np.isnan(Y), nan) and np.array_equal(bits(Y)[~nan], bits(Yr)[~nan])
+    plan, Y = _live_run(A, X, gpu)
+    assert plan.stats()["live_values"] and plan.stats()["tiled"]
+    assert same(Y, Yref)
+    odd = [r for r in range(1, m) if rp[r] % 2 == 1]
+    for r0, r1 in ((odd[0], 1500), (odd[len(odd) // 2], m), (odd[-1] - 200, m - 1)):
+        plan, Yb = _live_run(A, X, gpu, rows=(r0, r1))
+        assert same(Yb, Yref[r0:r1]), (r0, r1)
+
+
+def test_live_values_full_size_and_contract(gpu):
+    """The cop20k_A stand-ins at K = 32 and the stencil at K = 128: live
+    plans bit-identical; values changed IN PLACE with no bind are seen by the
+    next execute (live semantics: a bind is a no-op); inside a captured graph
+    too; and the live plan holds no snapshot."""
+    for A, K in ((smfv.cop20k_surrogate(), 32), (smfv.inputs.cop20k_irregular_surrogate(), 32),
+                 (smfv.cop20k_surrogate(), 128)):
+        X = smfv.generateLargeFatVector(A.numCols, K)
+        dA = smfv.DeviceCSR(A, gpu)
+        dX = torch.from_numpy(X).to(gpu)
+        live = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, live_values=True)
+        snap = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K)
+        st, ss = live.stats(), snap.stats()
+        assert st["live_values"] and st["tiled"] and st["tiles"] == ss["tiles"] and st["snapshot_entries"] == 0
+        Yl = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+        Ys = torch.full_like(Yl, np.nan)
+        live.run(dX, Yl)
+        snap.run(dX, Ys)
+        torch.cuda.synchronize()
+        assert torch.equal(Yl.view(torch.int64), Ys.view(torch.int64))
+        if K == 32 and A.numRows == 121192:
+            Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+            assert np.array_equal(bits(Yl.cpu().numpy()), bits(Yref))
+        # in place, no bind: the live plan's next execute reads the new values
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                rp, ci, va = dA.ptrs()
+                smfv._lib.call("smfv_plan_execute", live._plan, rp, ci, va, dX.data_ptr(), K, Yl.data_ptr(), K,
+                               S.stream_handle(side))
+        torch.cuda.current_stream().wait_stream(side)
+        dA.values.mul_(-0.5)
+        torch.cuda.synchronize()
+        g.replay()
+        snap.bind_values()  # (the snapshot plan needs its bind)
+        snap.run(dX, Ys)
+        torch.cuda.synchronize()
+        assert torch.equal(Yl.view(torch.int64), Ys.view(torch.int64))
+        del g
