@@ -1269,8 +1269,9 @@ def main() -> None:
         alt = [(plan.A.values, plan.A.values * 0.5 + 1.0) for plan, _, _ in copies]
         torch.cuda.synchronize()
 
-        def rb_step(i, execute=True):
+        def rb_step(i, execute=True, plans=None):
             plan, dX, dY = copies[i % ncopies]
+            plan = plan if plans is None else plans[i % ncopies]
             vals = alt[i % ncopies][(i // ncopies) % 2]
             st_ = torch.cuda.current_stream().cuda_stream
             _call("smfv_plan_bind_values", plan._plan, vals.data_ptr(), st_)
@@ -1290,6 +1291,28 @@ def main() -> None:
                   "timing": how_be,
                   "note": "every step binds its plan to values that changed since its last bind (two arrays "
                           "alternating per copy) and executes; bind_ms: the binds alone, same rotation"}
+        # (r5) the same with live-values plans (SMFV_PLAN_LIVE_VALUES: the
+        # tiled kernel reads the CSR values itself, a bind is a no-op) -- the
+        # plan a caller whose values change every product would take
+        if st0.get("kernel") == "k_rows_ws" and not st0.get("live_values"):
+            live = [smfv.SpmmPlan(smfv.Variant[variant], pl.A, K, tiles=args.tiles, fma=args.fma, seeds=args.seeds,
+                                  split_ends=args.split_ends, xcd_parts=args.xcd_parts,
+                                  tiled_kernel=args.tiled_kernel, live_values=True) for pl, _, _ in copies]
+            torch.cuda.synchronize()
+            if all(lp.stats()["live_values"] for lp in live):
+                ms_lbe, how_l = _graph_or_eager(lambda i: rb_step(i, True, live), args.steps, world)
+                rebind["live_values"] = {
+                    "bind_plus_execute_ms": round(ms_lbe, 6),
+                    "GFLOPs_incl_bind": round(2.0 * nnz * K / (ms_lbe * 1e-3) / 1e9, 3),
+                    "frac_incl_bind": round(prob_bytes / (ms_lbe * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                    "timing": how_l,
+                    "note": "live-values plans (SMFV_PLAN_LIVE_VALUES) of the same copies, same value changes: "
+                            "the bind is a no-op, the kernel DMAs each value pair from the CSR values"}
+                best = min(ms_be, ms_lbe)
+                rebind["best_bind_plus_execute_ms"] = round(best, 6)
+                rebind["best_plan"] = "live_values" if ms_lbe < ms_be else "snapshot"
+            del live
+            torch.cuda.synchronize()
     # the warm leg (same copy every launch) after the cold one; --no-warm
     # leaves it out so a profile of this process holds cold launches only
     span_ms_w = timed(capture(True)) if not args.no_warm else float("nan")

@@ -193,7 +193,13 @@ typedef struct smfv_plan_s *smfv_plan_t;
  * tiles of <= 64 rows and <= 239 staged X rows, 158 KiB of LDS); GEOM2 two
  * independent 512-lane blocks per CU (4 + 4 waves, tiles of <= 32 rows and
  * <= 125 X rows, 80 KiB of LDS each), so one block's per-tile hand-off hides
- * behind the other's work.  Same per-row order: bit-identical either way. */
+ * behind the other's work.  Same per-row order: bit-identical either way.
+ * Without a flag a plan takes GEOM1, except a SMALL plan (fewer than 1.5
+ * GEOM1 tiles per CU, e.g. a rank's row block at p = 8), which takes GEOM2
+ * when its 32-row tiles keep the re-use and add no direct rows: there one
+ * unit per block is all fill and drain, and half-size units halve it
+ * (7.9 -> 7.1 us on a cop20k rank block).  On whole cop20k GEOM2 is slower
+ * (2.6x the units: profiles/r04/ab_geom). */
 #define SMFV_PLAN_WS_GEOM1 1024
 #define SMFV_PLAN_WS_GEOM2 2048
 /* (r4) GEOM3: one 768-lane block per CU, 8 compute + 4 loader waves (16 X

@@ -607,7 +607,12 @@ struct WsXcd {
 // vidx[t * vstride + slot] of each slot (WsPlan::live): no snapshot, no bind
 template <int CW, int LW, int PPW, int UCAP, int NCAP, bool FMA = false, bool SADDR = true, bool NARROW = false,
           bool LIVE = false>
-__global__ __launch_bounds__(64 * (CW + LW), CW == 8 ? 1 : 2) void k_rows_ws(WsXcd xr, int npanel, int chunked,
+// (r5) the second bound is HIP's minimum waves per EU: geometry 2
+// runs two 512-lane blocks per CU = 4 waves per SIMD, so <= 128 VGPRs must
+// be forced (a 1024-lane block forces it by its size; 768 lanes: 3 waves,
+// 168 VGPRs allowed).  tests/test_host.py::test_ws_kernels_register_budget
+// reads the code object's VGPR counts.
+__global__ __launch_bounds__(64 * (CW + LW), CW == 4 ? 4 : 1) void k_rows_ws(WsXcd xr, int npanel, int chunked,
                                                      const int *__restrict__ grec,
                                                      const int *__restrict__ lrec,
                                                      const uint8_t *__restrict__ loff,

@@ -53,7 +53,9 @@ constexpr int WS_SLACK = 2048;   // entries past the end (DMA over-read of the l
 //             of LDS.
 //   WS_GEOM2: two 512-lane blocks per CU (4 + 4 waves), 32-row tiles, 80 KiB
 //             of LDS each: two independent two-slot pipelines per CU.
-//             Measured slower (2.6x the units; profiles/r04/ab_geom).
+//             Measured slower on whole matrices (2.6x the units;
+//             profiles/r04/ab_geom); the automatic choice for small plans
+//             (< 1.5 geometry-1 tiles per CU: smfv::plan_create).
 //   WS_GEOM3: one 768-lane block per CU (8 compute + 4 loader waves of 16
 //             pieces), 64-row tiles: 3 waves per SIMD, so a wave may hold up
 //             to 168 VGPRs and the compute waves run a deeper read-ahead.

@@ -589,3 +589,37 @@ def test_balanced_row_partition():
     ref = exchange_plan(1, m, A.nnz, A.rowPtr, K, p)
     wr = [work(int(ref[0][r]), int(ref[1][r]) + 1) for r in range(p)]
     assert max(wr) / (work(0, m) / p) > 1.02
+
+
+def test_ws_kernels_register_budget(tmp_path):
+    """(r5) Every k_rows_ws instance in libsmfv.so fits the waves
+    per SIMD its geometry runs: one 1024-lane block (geometry 1) or two
+    512-lane blocks (geometry 2) per CU = 4 waves per SIMD -> <= 128 VGPRs;
+    a 768-lane block (geometry 3) = 3 waves -> <= 168.  No spills.  Read from
+    the code object's metadata (llvm-objdump --offloading, llvm-readelf
+    --notes), so a compiler change that breaks the budget fails here."""
+    import re
+    import shutil
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(os.path.join(llvm, "llvm-readelf")):
+        pytest.skip("no ROCm llvm tools")
+    so = tmp_path / "libsmfv.so"
+    shutil.copy(os.path.join(PKG, "libsmfv.so"), so)
+    subprocess.run([os.path.join(llvm, "llvm-objdump"), "--offloading", str(so)], cwd=tmp_path, capture_output=True,
+                   check=True)
+    co = [f for f in os.listdir(tmp_path) if "gfx950" in f]
+    assert co, os.listdir(tmp_path)
+    notes = subprocess.run([os.path.join(llvm, "llvm-readelf"), "--notes", str(tmp_path / co[0])],
+                           capture_output=True, text=True, check=True).stdout
+    seen = 0
+    for blk in notes.split("  - .agpr_count:")[1:]:
+        name = re.search(r"\.name:\s+(\S+)", blk).group(1)
+        if "k_rows_ws" not in name:
+            continue
+        cw, lw = map(int, re.search(r"k_rows_wsILi(\d+)ELi(\d+)E", name).groups())
+        vgpr = int(re.search(r"\.vgpr_count:\s+(\d+)", blk).group(1))
+        spill = int(re.search(r"\.vgpr_spill_count:\s+(\d+)", blk).group(1))
+        waves_per_simd = 4 if (cw, lw) in ((8, 8), (4, 4)) else 3
+        assert vgpr <= 512 // waves_per_simd and spill == 0, (name, vgpr, spill)
+        seen += 1
+    assert seen >= 24, seen
