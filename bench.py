@@ -1118,9 +1118,10 @@ def main() -> None:
     ap.add_argument("--partition", default="reference", choices=["balanced", "reference"],
                     help="decomposed / --rank-plans ROWWISE: the reference's equal row counts (SC/...RowWise.cpp:26-29, "
                          "default) or row blocks of equal work (SMFV_DIST_BALANCED_ROWS)")
-    ap.add_argument("--chunks", type=int, default=2,
+    ap.add_argument("--chunks", type=int, default=1,
                     help="decomposed ROWWISE: also time the chunked exchange with this many row chunks per rank "
-                         "(SMFV_DIST_CHUNKS; 1 = skip)")
+                         "(SMFV_DIST_CHUNKS; 1 = skip, the default: its point-to-point RCCL groups have not run on "
+                         "more than one GPU yet, so the driver's run does not depend on them)")
     ap.add_argument("--rank-chunks", type=int, default=1,
                     help="--rank-plans ROWWISE: row chunks per rank plan (SMFV_DIST_CHUNKS; each chunk its own plan)")
     ap.add_argument("--xgmi-gbps", type=float, default=153.0,

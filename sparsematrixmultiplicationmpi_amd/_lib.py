@@ -157,7 +157,11 @@ def _load() -> ctypes.CDLL:
             "(make -C sparsematrixmultiplicationmpi_amd/csrc). There is no CPU fallback.")
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in _SIGS.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None and os.environ.get("SMFV_LIB"):
+            continue  # an older build loaded for an A/B run lacks newer entry points
+        if fn is None:
+            raise ImportError(f"{LIB_PATH} does not export {name}")
         fn.restype = res
         fn.argtypes = args
     return lib

@@ -813,7 +813,8 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 4 ? 4 : 1) void k_rows_ws(WsX
             const int blast = nbat + (rem ? 1 : 0) - 1;
             const u2 *Lq = reinterpret_cast<const u2 *>(mbase + M_L) + js + qk;
             const int vw = R[2 * L::R + slot];
-            const d2 *Vq = reinterpret_cast<const d2 *>(mbase + M_V) + (vw & 0xFFFF) + qk;
+            // (the LIVE flag bits sit above bit 16: a snapshot plan's word is the base itself)
+            const d2 *Vq = reinterpret_cast<const d2 *>(mbase + M_V) + (LIVE ? (vw & 0xFFFF) : vw) + qk;
             if constexpr (LIVE)
                 if (vw & (1 << 30)) {
                     // a row of odd length: its last pair's second half is the
