@@ -605,22 +605,14 @@ struct WsXcd {
 // (r5) LIVE: the loaders DMA the value pairs straight from the caller's CSR
 // values (tv = the block's first value, tv_bytes its bytes) at the CSR index
 // vidx[t * vstride + slot] of each slot (WsPlan::live): no snapshot, no bind
-template <int CW, int LW, int PPW, int UCAP, int NCAP, bool FMA = false, bool SADDR = true, bool NARROW = false,
-          bool LIVE = false>
-// (r5, ADVICE r4) the second bound is HIP's minimum waves per EU: geometry 2
-// runs two 512-lane blocks per CU = 4 waves per SIMD, so <= 128 VGPRs must
-// be forced (a 1024-lane block forces it by its size; 768 lanes: 3 waves,
-// 168 VGPRs allowed).  tests/test_host.py::test_ws_kernels_register_budget
-// reads the code object's VGPR counts.
-__global__ __launch_bounds__(64 * (CW + LW), CW == 4 ? 4 : 1) void k_rows_ws(WsXcd xr, int npanel, int chunked,
-                                                     const int *__restrict__ grec,
-                                                     const int *__restrict__ lrec,
-                                                     const uint8_t *__restrict__ loff,
-                                                     const double *__restrict__ tv,
-                                                     const double *__restrict__ X, int64_t ldx,
-                                                     double *__restrict__ Y, int64_t ldy,
-                                                     const int *__restrict__ vidx = nullptr, int vstride = 0,
-                                                     unsigned tv_bytes = 0)
+// The body is shared by the two kernels below: k_rows_ws (the snapshot,
+// with the r4 argument list) and k_rows_ws_live (r5, three more arguments).
+template <int CW, int LW, int PPW, int UCAP, int NCAP, bool FMA, bool SADDR, bool NARROW, bool LIVE>
+__device__ __forceinline__ void ws_body(int xfirst, int xend, int npanel, int chunked, const int *__restrict__ grec,
+                                        const int *__restrict__ lrec, const uint8_t *__restrict__ loff,
+                                        const double *__restrict__ tv, const double *__restrict__ X, int64_t ldx,
+                                        double *__restrict__ Y, int64_t ldy, const int *__restrict__ vidx,
+                                        int vstride, unsigned tv_bytes)
 {
     using namespace ws;
     using L = Lay<CW, LW, PPW, UCAP, NCAP>;
@@ -634,8 +626,8 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 4 ? 4 : 1) void k_rows_ws(WsX
         // chunked, as consecutive runs (block j: a run of q or q + 1 tiles),
         // so a block's next tile is the wavefront neighbour of its last one
         const int nb = gridDim.x >> 3;  // blocks per XCD
-        const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
-        const int first = xr.first[x], end = xr.first[x + 1];
+        const int j = blockIdx.x >> 3;
+        const int first = xfirst, end = xend;
         if (chunked & 1) {
             const int S = end - first, q = S / nb, r = S % nb;
             t0 = first + j * q + min(j, r);
@@ -941,32 +933,79 @@ __global__ __launch_bounds__(64 * (CW + LW), CW == 4 ? 4 : 1) void k_rows_ws(WsX
 }
 
 
+// (r5, ADVICE r4) the second bound is HIP's minimum waves per EU: geometry 2
+// runs two 512-lane blocks per CU = 4 waves per SIMD, so <= 128 VGPRs must
+// be forced (a 1024-lane block forces it by its size; 768 lanes: 3 waves,
+// 168 VGPRs allowed).  tests/test_host.py::test_ws_kernels_register_budget
+// reads the code object's VGPR counts.
+template <int CW, int LW, int PPW, int UCAP, int NCAP, bool FMA = false, bool SADDR = true, bool NARROW = false>
+__global__ __launch_bounds__(64 * (CW + LW), CW == 4 ? 4 : 1) void k_rows_ws(WsXcd xr, int npanel, int chunked,
+                                                     const int *__restrict__ grec,
+                                                     const int *__restrict__ lrec,
+                                                     const uint8_t *__restrict__ loff,
+                                                     const double *__restrict__ tv,
+                                                     const double *__restrict__ X, int64_t ldx,
+                                                     double *__restrict__ Y, int64_t ldy)
+{
+    // (the XCD's tile range read here, from the kernel arguments: scalar loads)
+    const int x = blockIdx.x & 7;
+    ws_body<CW, LW, PPW, UCAP, NCAP, FMA, SADDR, NARROW, false>(xr.first[x], xr.first[x + 1], npanel, chunked, grec,
+                                                               lrec, loff, tv, X, ldx, Y, ldy, nullptr, 0, 0u);
+}
+// (r5) live values: tv = the block's first CSR value, tv_bytes its bytes;
+// vidx[t * vstride + slot] the CSR index of each value slot (WsPlan::live)
+template <int CW, int LW, int PPW, int UCAP, int NCAP, bool FMA = false, bool NARROW = false>
+__global__ __launch_bounds__(64 * (CW + LW), CW == 4 ? 4 : 1) void k_rows_ws_live(WsXcd xr, int npanel, int chunked,
+                                                     const int *__restrict__ grec,
+                                                     const int *__restrict__ lrec,
+                                                     const uint8_t *__restrict__ loff,
+                                                     const double *__restrict__ tv,
+                                                     const double *__restrict__ X, int64_t ldx,
+                                                     double *__restrict__ Y, int64_t ldy,
+                                                     const int *__restrict__ vidx, int vstride, unsigned tv_bytes)
+{
+    const int x = blockIdx.x & 7;
+    ws_body<CW, LW, PPW, UCAP, NCAP, FMA, true, NARROW, true>(xr.first[x], xr.first[x + 1], npanel, chunked, grec, lrec,
+                                                             loff, tv, X, ldx, Y, ldy, vidx, vstride, tv_bytes);
+}
+
 // the product instances of k_rows_ws: geometry (smfv_plan.h WsGeom) x FMA x SADDR x NARROW
-#define SMFV_WS_INST(G_) k_rows_ws<G_.cw, G_.lw, G_.ppw, G_.ucap, G_.ncap, FMA, SADDR, NARROW, LIVE>
-template <bool FMA, bool SADDR, bool NARROW, bool LIVE> constexpr auto WS1 = SMFV_WS_INST(WS_GEOM1);
-template <bool FMA, bool SADDR, bool NARROW, bool LIVE> constexpr auto WS2 = SMFV_WS_INST(WS_GEOM2);
-template <bool FMA, bool SADDR, bool NARROW, bool LIVE> constexpr auto WS3 = SMFV_WS_INST(WS_GEOM3);
+#define SMFV_WS_INST(G_) k_rows_ws<G_.cw, G_.lw, G_.ppw, G_.ucap, G_.ncap, FMA, SADDR, NARROW>
+template <bool FMA, bool SADDR, bool NARROW> constexpr auto WS1 = SMFV_WS_INST(WS_GEOM1);
+template <bool FMA, bool SADDR, bool NARROW> constexpr auto WS2 = SMFV_WS_INST(WS_GEOM2);
+template <bool FMA, bool SADDR, bool NARROW> constexpr auto WS3 = SMFV_WS_INST(WS_GEOM3);
 #undef SMFV_WS_INST
-template <bool NARROW, bool LIVE>
+#define SMFV_WSL_INST(G_) k_rows_ws_live<G_.cw, G_.lw, G_.ppw, G_.ucap, G_.ncap, FMA, NARROW>
+template <bool FMA, bool NARROW> constexpr auto WSL1 = SMFV_WSL_INST(WS_GEOM1);
+template <bool FMA, bool NARROW> constexpr auto WSL2 = SMFV_WSL_INST(WS_GEOM2);
+template <bool FMA, bool NARROW> constexpr auto WSL3 = SMFV_WSL_INST(WS_GEOM3);
+#undef SMFV_WSL_INST
+template <bool NARROW>
 static auto pick_ws_n(int geom, bool fma, bool saddr)
 {
     if (geom == 2)
-        return fma ? (saddr ? WS2<true, true, NARROW, LIVE> : WS2<true, false, NARROW, LIVE>)
-                   : (saddr ? WS2<false, true, NARROW, LIVE> : WS2<false, false, NARROW, LIVE>);
+        return fma ? (saddr ? WS2<true, true, NARROW> : WS2<true, false, NARROW>)
+                   : (saddr ? WS2<false, true, NARROW> : WS2<false, false, NARROW>);
     if (geom == 3)
-        return fma ? (saddr ? WS3<true, true, NARROW, LIVE> : WS3<true, false, NARROW, LIVE>)
-                   : (saddr ? WS3<false, true, NARROW, LIVE> : WS3<false, false, NARROW, LIVE>);
-    return fma ? (saddr ? WS1<true, true, NARROW, LIVE> : WS1<true, false, NARROW, LIVE>)
-               : (saddr ? WS1<false, true, NARROW, LIVE> : WS1<false, false, NARROW, LIVE>);
+        return fma ? (saddr ? WS3<true, true, NARROW> : WS3<true, false, NARROW>)
+                   : (saddr ? WS3<false, true, NARROW> : WS3<false, false, NARROW>);
+    return fma ? (saddr ? WS1<true, true, NARROW> : WS1<true, false, NARROW>)
+               : (saddr ? WS1<false, true, NARROW> : WS1<false, false, NARROW>);
 }
-// (r4) narrow: a K = 4 / 8 / 16 window (one accumulator per lane); (r5) live:
-// value pairs DMA'd from the caller's CSR values (LIVE: SADDR always)
-static auto pick_ws(int geom, bool fma, bool saddr, bool narrow = false, bool live = false)
+// (r4) narrow: a K = 4 / 8 / 16 window (one accumulator per lane)
+static auto pick_ws(int geom, bool fma, bool saddr, bool narrow = false)
 {
-    if (live) return narrow ? pick_ws_n<true, true>(geom, fma, true) : pick_ws_n<false, true>(geom, fma, true);
-    return narrow ? pick_ws_n<true, false>(geom, fma, saddr) : pick_ws_n<false, false>(geom, fma, saddr);
+    return narrow ? pick_ws_n<true>(geom, fma, saddr) : pick_ws_n<false>(geom, fma, saddr);
 }
-
+// (r5) the live-values kernel (value pairs DMA'd from the caller's CSR; scalar-base addressing always)
+static auto pick_ws_live(int geom, bool fma, bool narrow)
+{
+    if (geom == 2)
+        return fma ? (narrow ? WSL2<true, true> : WSL2<true, false>) : (narrow ? WSL2<false, true> : WSL2<false, false>);
+    if (geom == 3)
+        return fma ? (narrow ? WSL3<true, true> : WSL3<true, false>) : (narrow ? WSL3<false, true> : WSL3<false, false>);
+    return fma ? (narrow ? WSL1<true, true> : WSL1<true, false>) : (narrow ? WSL1<false, true> : WSL1<false, false>);
+}
 
 // Rows the ws plan could not tile (over a cap alone): one 8-lane team per
 // row, X gathered straight from HBM, CSR order (bit-identical).  `rows` are
@@ -2558,26 +2597,32 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
         // snapshot each span < 4 GiB
         const bool saddr = (uint64_t)plan->n * (uint64_t)ldx * 8u < (1ull << 32) &&
                            (uint64_t)plan->snapshot * 8u < (1ull << 32);
-        auto kern = pick_ws(plan->ws_geom, plan->fma, saddr, false, plan->live);
+        auto kern = pick_ws(plan->ws_geom, plan->fma, saddr);
         WsXcd xr;
         for (int x = 0; x <= 8; ++x) xr.first[x] = plan->ws_xcd[x];
         const int threads = ws_geom(plan->ws_geom).threads();
         // (r4) K = 4 / 8 / 16: one panel, a narrow column window (chunked bits 16-23)
         const bool narrow = K < TILE_KP;
         if (narrow) {
-            kern = pick_ws(plan->ws_geom, plan->fma, saddr, true, plan->live);
+            kern = pick_ws(plan->ws_geom, plan->fma, saddr, true);
             chunked = (chunked & 1) | (K << 16);
         }
-        if (plan->live && !saddr) {
-            set_error("live-values tiled plan: X must span < 4 GiB (n * ldx * 8)");
-            return SMFV_ERR_INVALID;
+        if (plan->live) {
+            if (!saddr) {
+                set_error("live-values tiled plan: X must span < 4 GiB (n * ldx * 8)");
+                return SMFV_ERR_INVALID;
+            }
+            // the value pairs come from the block's CSR values through a
+            // range-checked buffer (the last odd row's read past the end gives 0)
+            hipLaunchKernelGGL(pick_ws_live(plan->ws_geom, plan->fma, narrow), dim3((unsigned)blocks),
+                               dim3((unsigned)threads), 0, st, xr, narrow ? 1 : K / TILE_KP, chunked, plan->ws_grec,
+                               plan->ws_lrec, plan->ws_loff, d_values + plan->nnz_base, d_X, ldx, d_Y, ldy,
+                               plan->ws_vidx, plan->ws_vstride, (unsigned)(plan->nnz * 8));
+        } else {
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3((unsigned)threads), 0, st, xr,
+                               narrow ? 1 : K / TILE_KP, chunked, plan->ws_grec, plan->ws_lrec, plan->ws_loff,
+                               plan->tvals, d_X, ldx, d_Y, ldy);
         }
-        // live: the value pairs come from the block's CSR values through a
-        // range-checked buffer (the last odd row's read past the end gives 0)
-        const double *tv = plan->live ? d_values + plan->nnz_base : plan->tvals;
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3((unsigned)threads), 0, st, xr,
-                           narrow ? 1 : K / TILE_KP, chunked, plan->ws_grec, plan->ws_lrec, plan->ws_loff, tv, d_X, ldx,
-                           d_Y, ldy, plan->ws_vidx, plan->ws_vstride, (unsigned)(plan->nnz * 8));
         SMFV_LAUNCHED();
     }
     if (plan->ndirect > 0) {

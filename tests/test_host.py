@@ -616,7 +616,7 @@ def test_ws_kernels_register_budget(tmp_path):
         name = re.search(r"\.name:\s+(\S+)", blk).group(1)
         if "k_rows_ws" not in name:
             continue
-        cw, lw = map(int, re.search(r"k_rows_wsILi(\d+)ELi(\d+)E", name).groups())
+        cw, lw = map(int, re.search(r"k_rows_ws(?:_live)?ILi(\d+)ELi(\d+)E", name).groups())
         vgpr = int(re.search(r"\.vgpr_count:\s+(\d+)", blk).group(1))
         spill = int(re.search(r"\.vgpr_spill_count:\s+(\d+)", blk).group(1))
         waves_per_simd = 4 if (cw, lw) in ((8, 8), (4, 4)) else 3
