@@ -240,6 +240,13 @@ SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_
  * parts (8 or 1), [7] X footprint of the 8 parts (-1: not computed),
  * [8] X footprint of the plan's 8 XCD tile ranges (distinct X rows each
  * reads, summed, over the block's distinct X rows).  No device needed. */
+/* (r5) The narrow-team plan of a kw = 4 / 8 column window (k_rows_wsn) for
+ * the row block [row_begin, row_end), built and verified on the host (the
+ * kernel's reads replayed): out[0] tiles, [1] staged X rows, [2] re-use,
+ * [3] direct rows, [4] rows of the fullest tile, [5] padded entries.  No
+ * device needed.  (SC/...ColumnWise.cpp:34-48 on a rank's K/p panel.) */
+SMFV_API int smfv_wsn_plan_analyse(int row_begin, int row_end, int n, const int *h_row_ptr,
+                                   const int *h_col_idx, int kw, double out[6]);
 SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int *h_row_ptr,
                                     const int *h_col_idx, int flags, double out[9]);
 /* The K = 1 chunk layout (k_spmv_chunks) of the row block [row_begin,
@@ -264,6 +271,7 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
  * rows per XCD, 1: one wavefront), [12] X rows the 8 parts read, summed,
  * over the pattern's X rows (-1: not computed), [13] the kernel a tiled
  * plan runs: 0 none (untiled), 1 k_rows_ws, 2 k_rows_mfma, 3 k_spmv_chunks,
+ * (r5) 5 k_rows_wsn (narrow-team tiles of a K = 4 / 8 window),
  * (4 was the retired k_rows_cs); [14] (r5) 1 if the tiled plan reads live
  * values (SMFV_PLAN_LIVE_VALUES), else 0; [15] (r4) the k_rows_ws
  * geometry (1: one 1024-lane block per CU, 2: two 512-lane blocks, 3: one

@@ -57,6 +57,7 @@ _SIGS = {
                                       c_int]),
     "smfv_plan_analyse": (c_int, [c_int, c_int, _PI, _PI, _PD]),
     "smfv_plan_analyse_rows": (c_int, [c_int, c_int, c_int, _PI, _PI, c_int, _PD]),
+    "smfv_wsn_plan_analyse": (c_int, [c_int, c_int, c_int, _PI, _PI, c_int, _PD]),
     "smfv_spmv_chunks_analyse": (c_int, [c_int, c_int, c_int, _PI, _PI, c_int, _PD]),
     "smfv_set_analysis_threads": (None, [c_int]),
     "smfv_plan_bind_values": (c_int, [c_void_p, c_void_p, c_void_p]),

@@ -1007,6 +1007,158 @@ static auto pick_ws_live(int geom, bool fma, bool narrow)
     return fma ? (narrow ? WSL1<true, true> : WSL1<true, false>) : (narrow ? WSL1<false, true> : WSL1<false, false>);
 }
 
+// ---------------------------------------------------------------------------
+// (r5) k_rows_wsn: the tiled row kernel for a NARROW column window of 4 or 8
+// columns (a ColumnWise rank's K/p panel, SC/...ColumnWise.cpp:34-48) on the
+// narrow-team plan (build_wsn_plan, smfv_plan.h WsnGeom).  One persistent
+// 1024-lane block per CU, 8 loader + 8 compute waves, two-slot pipeline as
+// k_rows_ws.  A team is KW/2 lanes (one double2 column pair each), so a
+// compute wave sums TW = 128/KW rows at once and a tile holds 256 (KW = 4) /
+// 128 (KW = 8) rows: 2-4 units per CU on cop20k where k_rows_ws's 64-row
+// tiles make 8.  The X image holds only the window (32 / 64 B per union row,
+// <= 1,023 / 639 rows, u16 image offsets).  Each row is summed in CSR order
+// with a separate multiply and add (bit-identical to the reference); pads
+// (zero image row, value -0.0) add +-0.
+// ---------------------------------------------------------------------------
+template <int KW> struct LayN {
+    static constexpr WsnGeom G = wsn_geom(KW);
+    static constexpr int TL = G.tl(), TW = G.tw(), R = G.rows(), XROW = G.xrow(), UCAP = G.ucap, NCAP = G.ncap;
+    static constexpr int XSLOT = (UCAP + 1) * XROW;
+    static constexpr int RP = 1024 / XROW;              // image rows per 1 KiB DMA piece
+    static constexpr int XPIECES = (UCAP + 1) / RP;
+    static constexpr int PPW = (XPIECES + WSN_LW - 1) / WSN_LW;
+    static constexpr int M_V = 0, M_L = NCAP * 8, M_R = M_L + NCAP * 2;
+    static constexpr int RECB = G.lwords() * 4;
+    static constexpr int RECP = (RECB + 1023) / 1024;   // record DMA pieces
+    static constexpr int MSLOT = (M_R + RECP * 1024 + 1023) / 1024 * 1024;
+    static constexpr int SL_M = 2 * XSLOT;
+    static constexpr int BYTES = SL_M + 2 * MSLOT;
+    static_assert(BYTES <= 160 * 1024, "two X images and two meta slots fit the CU's 160 KiB");
+    static_assert((UCAP + 1) % RP == 0 && XSLOT % 1024 == 0 && M_L % 1024 == 0 && M_R % 1024 == 0, "1 KiB pieces");
+    static_assert(G.lwords() <= WSN_GWORDS, "record");
+};
+
+template <int KW, bool FMA>
+__global__ __launch_bounds__(1024, 1) void k_rows_wsn(WsXcd xr, const int *__restrict__ grec,
+                                                      const int *__restrict__ lrec,
+                                                      const uint16_t *__restrict__ loff,
+                                                      const double *__restrict__ tv,
+                                                      const double *__restrict__ X, int64_t ldx,
+                                                      double *__restrict__ Y, int64_t ldy)
+{
+    using namespace ws;
+    using L = LayN<KW>;
+    constexpr int TL = L::TL, TW = L::TW, R = L::R, XROW = L::XROW, UCAP = L::UCAP;
+    __shared__ __attribute__((aligned(16))) char lds[L::BYTES];
+    const int nb = gridDim.x >> 3, x = blockIdx.x & 7, jb = blockIdx.x >> 3;
+    const int first = xr.first[x], end = xr.first[x + 1];
+    const int t0 = first + jb;
+    if (t0 >= end) return;  // block-uniform
+    const int cnt = (end - 1 - t0) / nb + 1;
+    const int tlast = t0 + (cnt - 1) * nb;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const unsigned lds0 = (unsigned)(uintptr_t)lds;
+    if (wv >= 8) {
+        // ---------------- loader waves ----------------
+        __builtin_amdgcn_s_setprio(3);
+        const int wl = wv - 8;
+        if (wl == 0 && lane < 2 * (XROW / 16))  // the zero image row of both X slots
+            reinterpret_cast<d2 *>(lds + (lane / (XROW / 16)) * L::XSLOT + UCAP * XROW)[lane % (XROW / 16)] =
+                d2{0.0, 0.0};
+        int uid[L::PPW];
+        int noff, tn, nu, voff, tnv;
+        const unsigned ldxb = (unsigned)(ldx * 8);
+        auto fetch_record = [&](int t) {
+            const int *Gr = grec + (int64_t)t * WSN_GWORDS;
+#pragma unroll
+            for (int i = 0; i < L::PPW; ++i) {
+                const int piece = wl + WSN_LW * i;
+                uid[i] = piece < L::XPIECES ? Gr[L::RP * piece + lane / TL] : 0;
+            }
+            noff = Gr[WSN_G_NOFF + (lane & 15)];
+            tn = Gr[WSN_G_TN + (lane & 15)];
+            nu = Gr[WSN_G_NU + (lane & 15)];
+            voff = Gr[WSN_G_VOFF + (lane & 15)];
+            tnv = Gr[WSN_G_TNV + (lane & 15)];
+        };
+        auto stage = [&](int t, int slot) {
+#pragma unroll
+            for (int i = 0; i < L::PPW; ++i) asm volatile("" ::"v"(uid[i]));
+            asm volatile("" ::"v"(noff), "v"(tn), "v"(nu), "v"(voff), "v"(tnv));
+            const unsigned xb = lds0 + slot * L::XSLOT;
+#pragma unroll
+            for (int i = 0; i < L::PPW; ++i) {
+                const int piece = wl + WSN_LW * i;
+                // a lane stages its 16 B of image row RP piece + lane / TL (never the zero row: nu <= UCAP)
+                if (piece < L::XPIECES && L::RP * piece + lane / TL < nu)
+                    dma16s<false>(X, (unsigned)uid[i] * ldxb + 16u * (unsigned)(lane % TL), xb + piece * 1024);
+            }
+            const unsigned mb = lds0 + L::SL_M + slot * L::MSLOT;
+            const double *tvb = tv + __builtin_amdgcn_readfirstlane(voff);
+            const uint16_t *lb = loff + __builtin_amdgcn_readfirstlane(noff);
+            for (int k = wl; k * 128 < tnv; k += WSN_LW) dma16s<true>(tvb, 1024u * k + 16u * lane, mb + L::M_V + k * 1024);
+            for (int k = wl; k * 512 < tn; k += WSN_LW) dma16s<true>(lb, 1024u * k + 16u * lane, mb + L::M_L + k * 1024);
+#pragma unroll
+            for (int k = 0; k < L::RECP; ++k)
+                if (wl == WSN_LW - 1 - k && 16 * lane + 1024 * k < L::RECB)
+                    dma16s<true>(lrec + (int64_t)t * L::G.lwords(), 1024u * k + 16u * lane, mb + L::M_R + k * 1024);
+        };
+        fetch_record(t0);
+        stage(t0, 0);
+        fetch_record(min(t0 + nb, tlast));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_lds();
+        for (int u = 0; u < cnt; ++u) {
+            if (u + 1 < cnt) {
+                const int t = t0 + (u + 1) * nb;
+                stage(t, (u + 1) & 1);
+                fetch_record(min(t + nb, tlast));
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // unit u + 1 has landed
+            barrier_lds();
+        }
+        return;
+    }
+    // ---------------- compute waves ----------------
+    auto madd = [](d2 a, double v, d2 xx) -> d2 {
+        if constexpr (FMA)
+            return d2{__builtin_fma(v, xx.x, a.x), __builtin_fma(v, xx.y, a.y)};
+        else
+            return a + v * xx;
+    };
+    const int k = lane / TL, tli = lane % TL;
+    barrier_lds();
+    for (int u = 0; u < cnt; ++u) {
+        const char *xbase = lds + (u & 1) * L::XSLOT + 16 * tli;
+        const char *mbase = lds + L::SL_M + (u & 1) * L::MSLOT;
+        const int *RR = reinterpret_cast<const int *>(mbase + L::M_R);
+        const int word = RR[wv * TW + k];
+        if (word != -1) {
+            const int row = word & 0xFFFFFF, nbat = (int)((unsigned)word >> 24);
+            const u4 *Lq = reinterpret_cast<const u4 *>(mbase + L::M_L) + RR[R + 2 * wv] + k;
+            const d2 *Vq = reinterpret_cast<const d2 *>(mbase + L::M_V) + RR[R + 2 * wv + 1] + k;
+            d2 acc = {0.0, 0.0};
+            u4 ow = Lq[0];
+            for (int b = 0; b < nbat; ++b) {
+                d2 v[4], xx[8];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = Vq[(4 * b + q) * TW];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const unsigned w32 = e < 2 ? ow.x : e < 4 ? ow.y : e < 6 ? ow.z : ow.w;
+                    const unsigned off = (e & 1) ? (w32 >> 16) : (w32 & 0xFFFFu);
+                    xx[e] = *reinterpret_cast<const d2 *>(xbase + off * XROW);
+                }
+                if (b + 1 < nbat) ow = Lq[(b + 1) * TW];  // the next batch's offsets behind this batch's reads
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc = madd(acc, (e & 1) ? v[e >> 1].y : v[e >> 1].x, xx[e]);
+            }
+            __builtin_nontemporal_store(acc, reinterpret_cast<d2 *>(Y + (int64_t)row * ldy + 2 * tli));
+        }
+        barrier_lds();  // X slot (u & 1) and meta slot (u & 1) are free for unit u + 2
+    }
+}
+
 // Rows the ws plan could not tile (over a cap alone): one 8-lane team per
 // row, X gathered straight from HBM, CSR order (bit-identical).  `rows` are
 // block-local (Y row), row_begin + row indexes the CSR; the values come from
@@ -1893,6 +2045,9 @@ struct smfv_plan_s {
     int *bind_items = nullptr;             // (r4) 2 ints per bind item (k_bind_items)
     int64_t nbind_items = 0;
     bool bind_desc = false;                // bind by k_bind_items (pads filled at creation)
+    bool wsn = false;                      // (r5) k_rows_wsn: narrow-team tiles for a 4 / 8-column window
+    int *wsn_grec = nullptr, *wsn_lrec = nullptr;
+    uint16_t *wsn_loff = nullptr;
     bool live = false;                     // (r5) k_rows_ws reads the live CSR values (ws_vidx): no snapshot
     int *ws_vidx = nullptr;                // live: per tile value slot, its first entry's block-local CSR index
     int ws_vstride = 0;
@@ -1927,7 +2082,8 @@ struct smfv_plan_s {
     ~smfv_plan_s()
     {
         delete sub;
-        for (void *q : {(void *)tsrc, (void *)bind_items, (void *)tvals, (void *)ws_vidx, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
+        for (void *q : {(void *)tsrc, (void *)bind_items, (void *)tvals, (void *)ws_vidx, (void *)wsn_grec, (void *)wsn_lrec,
+                        (void *)wsn_loff, (void *)ws_grec, (void *)ws_lrec, (void *)direct_rows,
                         (void *)direct_off, (void *)ws_loff, ws, (void *)mf_rec, (void *)mf_ucols, (void *)mf_bstep,
                         (void *)k1_hdr, (void *)k1_rs, (void *)k1_off, (void *)k1_col, (void *)cs_bs,
                         (void *)cs_trow, (void *)cs_tlast, (void *)cs_crec, (void *)cs_aux})
@@ -2120,7 +2276,52 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
                 }
             }
         }
-        if (!rc && go && !p->mfma && !(flags & SMFV_PLAN_MFMA)) {
+        // (r5) a 4- or 8-column window (a ColumnWise rank's panel): the
+        // narrow-team tiles of k_rows_wsn, 2-4x the rows of a k_rows_ws tile
+        // (SMFV_PLAN_WS keeps k_rows_ws's NARROW form, A/B)
+        if (!rc && go && !p->mfma && !(flags & (SMFV_PLAN_MFMA | SMFV_PLAN_WS | SMFV_PLAN_LIVE_VALUES)) &&
+            (K == 4 || K == 8)) {
+            WsnPlan Wn;
+            std::string err;
+            TileCaps cn = caps;
+            if (build_wsn_plan(m, n, rpl.data(), cil, K, Wn, &err, cn) && Wn.ntiles > 0 && Wn.union_rows > 0 &&
+                ((double)Wn.tiled_nnz / (double)Wn.union_rows >= SMFV_TILE_MIN_REUSE ||
+                 (flags & SMFV_PLAN_FORCE_TILES))) {
+                p->tiled = p->wsn = true;
+                p->ntiles = Wn.ntiles;
+                for (int x = 0; x <= 8; ++x) p->ws_xcd[x] = Wn.xcd[x];
+                p->parts = caps.part_start.size() > 2 ? (int)caps.part_start.size() - 1 : 1;
+                p->union_rows = Wn.union_rows;
+                p->tiled_nnz = Wn.tiled_nnz;
+                p->padded_nnz = Wn.ventries;
+                p->ndirect = (int)Wn.direct.size();
+                p->reuse = (double)Wn.tiled_nnz / (double)Wn.union_rows;
+                std::vector<int> &ts = Wn.tsrc;
+                for (int &q : ts)
+                    if (q >= 0) q += (int)nnz_base;
+                std::vector<int64_t> doff;
+                for (int r : Wn.direct) {
+                    if (ts.size() % 2) ts.push_back(-1);
+                    doff.push_back((int64_t)ts.size());
+                    for (int j = rpl[r]; j < rpl[r + 1]; ++j) ts.push_back((int)(nnz_base + j));
+                }
+                p->snapshot = (int64_t)ts.size();
+                if (!rc) rc = upload(&p->wsn_grec, Wn.grec, p->dev_bytes);
+                if (!rc) rc = upload(&p->wsn_lrec, Wn.lrec, p->dev_bytes);
+                if (!rc) rc = upload(&p->wsn_loff, Wn.loff, p->dev_bytes);
+                if (!rc) rc = upload(&p->direct_rows, Wn.direct, p->dev_bytes);
+                if (!rc) rc = upload(&p->direct_off, doff, p->dev_bytes);
+                // (the per-entry gather binds it: a team's value pairs are TW
+                // chunks apart, not the 4 / 1 the bind items know)
+                if (!rc) rc = upload(&p->tsrc, ts, p->dev_bytes);
+                if (!rc) {
+                    const size_t b = std::max<size_t>((size_t)p->snapshot, 1) * sizeof(double);
+                    fail_hip(hipMalloc(reinterpret_cast<void **>(&p->tvals), b), "hipMalloc(tvals)");
+                    p->dev_bytes += b;
+                }
+            }
+        }
+        if (!rc && go && !p->mfma && !p->wsn && !(flags & SMFV_PLAN_MFMA)) {
             WsPlan W;
             std::string err;
             // a pattern the tile layout cannot take (the replayed plan fails its
@@ -2321,6 +2522,40 @@ SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_
     return rc;
 }
 
+SMFV_API int smfv_wsn_plan_analyse(int row_begin, int row_end, int n, const int *h_row_ptr_all,
+                                   const int *h_col_idx_all, int kw, double out[6])
+{
+    SMFV_REQUIRE(row_begin >= 0 && row_end >= row_begin && n >= 0 && h_row_ptr_all && h_col_idx_all && out &&
+                     (kw == 4 || kw == 8),
+                 "bad argument");
+    const int m = row_end - row_begin;
+    std::vector<int> rpl((size_t)m + 1);
+    for (int i = 0; i <= m; ++i) rpl[i] = h_row_ptr_all[row_begin + i] - h_row_ptr_all[row_begin];
+    const int *cil = h_col_idx_all + h_row_ptr_all[row_begin];
+    TileCaps caps = plan_caps(0, row_begin);
+    double footprint = -1.0;
+    plan_parts(caps, 0, m, n, rpl.data(), cil, &footprint);
+    WsnPlan W;
+    std::string err;
+    if (!build_wsn_plan(m, n, rpl.data(), cil, kw, W, &err, caps)) {
+        set_error("%s", err.c_str());
+        return SMFV_ERR_INVALID;
+    }
+    int64_t most = 0;  // rows of the fullest tile
+    for (int t = 0; t < W.ntiles; ++t) {
+        int64_t r = 0;
+        for (int s = 0; s < W.geom.rows(); ++s) r += W.lrec[(size_t)t * W.geom.lwords() + s] != -1;
+        most = std::max(most, r);
+    }
+    out[0] = W.ntiles;
+    out[1] = (double)W.union_rows;
+    out[2] = W.union_rows ? (double)W.tiled_nnz / (double)W.union_rows : 0.0;
+    out[3] = (double)W.direct.size();
+    out[4] = (double)most;
+    out[5] = (double)W.entries;
+    return SMFV_OK;
+}
+
 SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int *h_row_ptr_all,
                                     const int *h_col_idx_all, int flags, double out[9])
 {
@@ -2502,9 +2737,9 @@ SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS])
     out[10] = plan->mfma ? 1.0 : 0.0;
     out[11] = plan->parts;
     out[12] = plan->footprint;
-    out[13] = !plan->tiled ? 0.0 : plan->k1 ? 3.0 : plan->mfma ? 2.0 : 1.0;
+    out[13] = !plan->tiled ? 0.0 : plan->k1 ? 3.0 : plan->mfma ? 2.0 : plan->wsn ? 5.0 : 1.0;
     out[14] = plan->live ? 1.0 : 0.0;  // (r5) live values (k_rows_cs, which used this slot, is retired)
-    out[15] = plan->tiled && !plan->k1 && !plan->mfma ? plan->ws_geom : 0;
+    out[15] = plan->tiled && !plan->k1 && !plan->mfma && !plan->wsn ? plan->ws_geom : 0;
     out[16] = plan->bind_desc ? 1.0 : 0.0;
     return SMFV_OK;
 }
@@ -2587,6 +2822,18 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
                                plan->mf_ucols, plan->mf_bstep, plan->tvals, d_X, ldx, d_Y, ldy);
             SMFV_LAUNCHED();
         }
+    } else if (plan->wsn && plan->ntiles > 0) {
+        // (r5) narrow-team tiles: one persistent 1024-lane block per CU
+        if ((uint64_t)plan->n * (uint64_t)ldx * 8u >= (1ull << 32) || (uint64_t)plan->snapshot * 8u >= (1ull << 32))
+            return launch_rows(plan->row_begin, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, plan->n, K, d_Y, ldy, st);
+        WsXcd xr;
+        for (int x = 0; x <= 8; ++x) xr.first[x] = plan->ws_xcd[x];
+        const int blocks = std::max(8, (std::min(plan->ntiles, ncu) + 7) & ~7);
+        auto kern = K == 4 ? (plan->fma ? k_rows_wsn<4, true> : k_rows_wsn<4, false>)
+                           : (plan->fma ? k_rows_wsn<8, true> : k_rows_wsn<8, false>);
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(1024), 0, st, xr, plan->wsn_grec, plan->wsn_lrec,
+                           plan->wsn_loff, plan->tvals, d_X, ldx, d_Y, ldy);
+        SMFV_LAUNCHED();
     } else if (plan->ntiles > 0) {
         // persistent blocks: one (geometry 1) or two (geometry 2) per CU; a
         // multiple of 8 (>= 8) so every XCD's tile range has blocks

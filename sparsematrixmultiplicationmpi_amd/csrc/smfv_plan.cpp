@@ -976,3 +976,247 @@ bool build_spmv_chunks(int m, int n, const int *rp, const int *ci, int cap, int 
 }
 
 }  // namespace smfv
+
+// ---------------------------------------------------------------------------
+// (r5) k_rows_wsn plan: narrow-team tiles for a 4- / 8-column window
+// ---------------------------------------------------------------------------
+namespace smfv {
+
+namespace {
+// Replays k_rows_wsn's reads for every tile: each row's entries must come out
+// as its CSR non-zeros in order, then pads (zero image row, value -0.0).
+bool verify_wsn_plan(int m, int n, const int *rp, const int *ci, const WsnPlan &P, std::string *err)
+{
+    auto fail = [&](const std::string &msg) {
+        if (err) *err = "wsn plan: " + msg;
+        return false;
+    };
+    const WsnGeom G = P.geom;
+    const int R = G.rows(), TW = G.tw(), LWD = G.lwords();
+    std::vector<char> seen((size_t)std::max(m, 1), 0);
+    for (int r : P.direct) {
+        if (r < 0 || r >= m || seen[r]) return fail("direct row out of range or repeated");
+        seen[r] = 1;
+    }
+    if ((int64_t)P.loff.size() != P.entries + WS_SLACK || (int64_t)P.tsrc.size() != P.ventries + WS_SLACK)
+        return fail("entry arrays");
+    for (int t = 0; t < P.ntiles; ++t) {
+        const int *g = &P.grec[(size_t)t * WSN_GWORDS];
+        const int *l = &P.lrec[(size_t)t * LWD];
+        const int noff = g[WSN_G_NOFF], tn = g[WSN_G_TN], nu = g[WSN_G_NU], voff = g[WSN_G_VOFF], tnv = g[WSN_G_TNV];
+        for (int q = 0; q < 16; ++q)
+            if (g[WSN_G_NOFF + q] != noff || g[WSN_G_TN + q] != tn || g[WSN_G_NU + q] != nu ||
+                g[WSN_G_VOFF + q] != voff || g[WSN_G_TNV + q] != tnv)
+                return fail("record header not replicated");
+        if (noff % 8 || tn % 8 || tn <= 0 || tn > G.ncap || nu < 0 || nu > G.ucap || voff % 8 || tnv != tn ||
+            (int64_t)noff + tn > P.entries || (int64_t)voff + tnv > P.ventries)
+            return fail("tile header out of range");
+        for (int u = 0; u < 1024; ++u)
+            if (g[u] < 0 || g[u] >= std::max(n, 1) || (u >= nu && g[u] != 0)) return fail("union id out of range");
+        for (int w = 0; w < 8; ++w) {
+            const int lb = l[R + 2 * w], vb = l[R + 2 * w + 1];
+            for (int k = 0; k < TW; ++k) {
+                const int word = l[w * TW + k];
+                if (word == -1) continue;
+                const int r = word & 0xFFFFFF, nbat = (int)((unsigned)word >> 24);
+                if (r < 0 || r >= m || seen[r]) return fail("tile row out of range or repeated");
+                seen[r] = 1;
+                const int rl = rp[r + 1] - rp[r];
+                if (nbat != std::max(1, (rl + 7) / 8)) return fail("row batches");
+                for (int b = 0; b < nbat; ++b)
+                    for (int e = 0; e < 8; ++e) {
+                        const int el = 8 * b + e;
+                        const int64_t le = (int64_t)noff + 8 * (int64_t)(lb + b * TW + k) + e;
+                        const int64_t ve = (int64_t)voff + 2 * (int64_t)(vb + (4 * b + e / 2) * TW + k) + e % 2;
+                        if (le >= noff + tn || ve >= voff + tnv) return fail("segment leaves its tile");
+                        if (el < rl) {
+                            const int j = rp[r] + el, u = P.loff[(size_t)le];
+                            if (P.tsrc[(size_t)ve] != j || u >= nu || g[u] != ci[j])
+                                return fail("row entry is not its CSR non-zero");
+                        } else if (P.tsrc[(size_t)ve] != -1 || P.loff[(size_t)le] != G.ucap) {
+                            return fail("pad entry does not read the zero row");
+                        }
+                    }
+            }
+        }
+    }
+    for (int r = 0; r < m; ++r)
+        if (!seen[r]) return fail("row " + std::to_string(r) + " in no tile");
+    return true;
+}
+}  // namespace
+
+namespace {
+bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPlan &P, std::string *err,
+                       const TileCaps &caps_in, int frac_num, int frac_den)
+{
+    P = WsnPlan();
+    if (kw != 4 && kw != 8) {
+        if (err) *err = "wsn plan: window must be 4 or 8 columns";
+        return false;
+    }
+    const WsnGeom G = wsn_geom(kw);
+    P.geom = G;
+    const int TW = G.tw(), R = G.rows(), LWD = G.lwords();
+    TileCaps caps = caps_in;
+    caps.ucap = G.ucap;
+    caps.maxrows = R;
+    caps.pad = 8;
+    // the analysis counts each row padded to 8; the layout pads a wave's rows
+    // to its longest, so the analysis aims below the cap and the layout
+    // checks the real figure (splitting a tile that still overflows)
+    caps.ncap = G.ncap * frac_num / frac_den;
+    TileAnalysis T;
+    analyse_tiles(m, n, rp, ci, T, caps);
+
+    auto nbat = [&](int r) { return std::max(1, (rp[r + 1] - rp[r] + 7) / 8); };
+    auto by_length = [&](std::vector<int> &rows) {
+        std::sort(rows.begin(), rows.end(), [&](int a, int b) {
+            const int la = rp[a + 1] - rp[a], lb = rp[b + 1] - rp[b];
+            return la != lb ? la > lb : a < b;
+        });
+    };
+    auto layout = [&](const std::vector<int> &rows) {  // padded entries (rows sorted by decreasing length)
+        int64_t e = 0;
+        for (size_t g = 0; g < rows.size(); g += (size_t)TW) e += (int64_t)nbat(rows[g]) * TW * 8;
+        return e;
+    };
+    std::vector<std::vector<int>> tiles, stack;
+    const int np = (int)T.part_tile.size() - 1;
+    std::vector<int> first_tile((size_t)np + 1, 0);
+    for (size_t t = 0, part = 0; t < T.meta.size(); ++t) {
+        while ((int)part < np && (int)t >= T.part_tile[part + 1]) first_tile[++part] = (int)tiles.size();
+        const TileMeta &tm = T.meta[t];
+        std::vector<int> rows(T.grow.begin() + tm.roff, T.grow.begin() + tm.roff + tm.nrows);
+        if (tm.direct) {
+            P.direct.insert(P.direct.end(), rows.begin(), rows.end());
+            continue;
+        }
+        by_length(rows);
+        stack.assign(1, rows);
+        while (!stack.empty()) {
+            std::vector<int> Rw = std::move(stack.back());
+            stack.pop_back();
+            if (layout(Rw) <= G.ncap && nbat(Rw[0]) <= 255) {
+                tiles.push_back(std::move(Rw));
+            } else if (Rw.size() == 1) {
+                P.direct.push_back(Rw[0]);
+            } else {
+                const size_t h = Rw.size() / 2;
+                stack.emplace_back(Rw.begin() + h, Rw.end());
+                stack.emplace_back(Rw.begin(), Rw.begin() + h);
+            }
+        }
+    }
+    for (int x = 1; x <= np; ++x)
+        if (x == np || T.part_tile[x] >= (int)T.meta.size()) first_tile[x] = std::max(first_tile[x], (int)tiles.size());
+    const int64_t N = (int64_t)tiles.size();
+    for (int x = 0; x <= 8; ++x) P.xcd[x] = np == 8 ? first_tile[x] : (int)(N * x / 8);
+    if (np == 8 && N > 0) {  // no XCD runs a round more than the tile count needs (as build_ws_plan)
+        const int64_t nbk = std::max(1, caps.xcd_blocks);
+        const int64_t cap = nbk * ((N + 8 * nbk - 1) / (8 * nbk));
+        for (int x = 1; x < 8; ++x)
+            P.xcd[x] = (int)std::max<int64_t>(std::min<int64_t>(P.xcd[x], P.xcd[x - 1] + cap),
+                                              std::max<int64_t>(N - cap * (8 - x), P.xcd[x - 1]));
+    }
+    const int nt = (int)N;
+    std::vector<int64_t> toff((size_t)nt + 1, 0);
+    for (int t = 0; t < nt; ++t) toff[(size_t)t + 1] = toff[(size_t)t] + layout(tiles[(size_t)t]);
+    P.ntiles = nt;
+    P.entries = P.ventries = toff[(size_t)nt];
+    if (P.entries + WS_SLACK > 0x7fffffff) {
+        if (err) *err = "wsn plan: too many tile entries for int32 offsets";
+        return false;
+    }
+    P.loff.assign((size_t)(P.entries + WS_SLACK), (uint16_t)G.ucap);
+    P.tsrc.assign((size_t)(P.ventries + WS_SLACK), -1);
+    P.grec.assign((size_t)nt * WSN_GWORDS, 0);
+    P.lrec.assign((size_t)nt * LWD, 0);
+    std::vector<int> pos((size_t)std::max(n, 1), -1), ucols;
+    for (int t = 0; t < nt; ++t) {
+        const std::vector<int> &Rw = tiles[(size_t)t];
+        const int64_t noff = toff[(size_t)t];
+        ucols.clear();
+        for (int r : Rw)
+            for (int j = rp[r]; j < rp[r + 1]; ++j)
+                if (pos[ci[j]] < 0) {
+                    pos[ci[j]] = (int)ucols.size();
+                    ucols.push_back(ci[j]);
+                }
+        const int nu = (int)ucols.size();
+        int *g = &P.grec[(size_t)t * WSN_GWORDS];
+        int *l = &P.lrec[(size_t)t * LWD];
+        for (int u = 0; u < nu; ++u) g[u] = ucols[(size_t)u];
+        for (int s = 0; s < R; ++s) l[s] = -1;
+        // wave group q (TW consecutive rows of the sorted list) -> wave w;
+        // groups q and 7 - q share a SIMD (waves w and w + 4)
+        int64_t chunk = 0;  // 16-byte offset chunks so far (= 8 entries each)
+        int lbase[8] = {}, vbase[8] = {}, wnb[8] = {};
+        for (int q = 0; q < 8 && (size_t)q * TW < Rw.size(); ++q) {
+            const int w = q < 4 ? q : 11 - q;
+            wnb[w] = nbat(Rw[(size_t)q * TW]);
+        }
+        int64_t vchunk = 0;
+        for (int w = 0; w < 8; ++w) {
+            lbase[w] = (int)chunk;
+            vbase[w] = (int)vchunk;
+            chunk += (int64_t)wnb[w] * TW;
+            vchunk += (int64_t)wnb[w] * 4 * TW;
+        }
+        for (int q = 0; q < 8 && (size_t)q * TW < Rw.size(); ++q) {
+            const int w = q < 4 ? q : 11 - q;
+            for (int k = 0; k < TW && (size_t)(q * TW + k) < Rw.size(); ++k) {
+                const int r = Rw[(size_t)(q * TW + k)];
+                l[w * TW + k] = r | (nbat(r) << 24);
+                for (int j = rp[r]; j < rp[r + 1]; ++j) {
+                    const int el = j - rp[r], b = el / 8, e = el % 8;
+                    P.loff[(size_t)(noff + 8 * (int64_t)(lbase[w] + b * TW + k) + e)] = (uint16_t)pos[ci[j]];
+                    P.tsrc[(size_t)(noff + 2 * (int64_t)(vbase[w] + (4 * b + e / 2) * TW + k) + e % 2)] = j;
+                }
+                P.tiled_nnz += rp[r + 1] - rp[r];
+            }
+        }
+        for (int w = 0; w < 8; ++w) {
+            l[R + 2 * w] = lbase[w];
+            l[R + 2 * w + 1] = vbase[w];
+        }
+        for (int q = 0; q < 16; ++q) {
+            g[WSN_G_NOFF + q] = (int)noff;
+            g[WSN_G_TN + q] = (int)(toff[(size_t)t + 1] - noff);
+            g[WSN_G_NU + q] = nu;
+            g[WSN_G_VOFF + q] = (int)noff;
+            g[WSN_G_TNV + q] = (int)(toff[(size_t)t + 1] - noff);
+        }
+        for (int c : ucols) pos[c] = -1;
+        P.union_rows += nu;
+    }
+    std::sort(P.direct.begin(), P.direct.end());
+    return verify_wsn_plan(m, n, rp, ci, P, err);
+}
+}  // namespace
+
+// The analysis aims at a fraction of the entry cap (it counts each row
+// padded to 8, the layout pads a wave's rows to its longest, and a tile that
+// still overflows is split in halves); the best fraction depends on the
+// row-length spread (cop20k stand-ins, tiles at 3/4 .. 9/10: 884-975 /
+// 1,095-1,294 stencil, 1,110-1,319 / 1,449-1,612 irregular at K = 4 / 8),
+// so four are built and the plan with the fewest tiles is kept.
+bool build_wsn_plan(int m, int n, const int *rp, const int *ci, int kw, WsnPlan &P, std::string *err,
+                    const TileCaps &caps)
+{
+    static constexpr int fr[4][2] = {{3, 4}, {13, 16}, {7, 8}, {9, 10}};
+    bool any = false;
+    for (const auto &f : fr) {
+        WsnPlan Q;
+        std::string e;
+        if (!build_wsn_plan_at(m, n, rp, ci, kw, Q, &e, caps, f[0], f[1])) {
+            if (err && !any) *err = e;
+            continue;
+        }
+        if (!any || Q.ntiles < P.ntiles || (Q.ntiles == P.ntiles && Q.union_rows < P.union_rows)) P = std::move(Q);
+        any = true;
+    }
+    return any;
+}
+
+}  // namespace smfv

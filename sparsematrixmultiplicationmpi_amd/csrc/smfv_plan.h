@@ -190,6 +190,57 @@ double parts_footprint(int m, int n, const int *row_ptr, const int *col_idx, con
                        const std::vector<int> &start);
 
 // ---------------------------------------------------------------------------
+// (r5) Plan of the narrow-team tiled kernel k_rows_wsn: a 4- or 8-column
+// window (a ColumnWise rank's K/p panel, SC/...ColumnWise.cpp:25-48).  A
+// team is KW/2 lanes (one double2 column pair each), so a wave holds
+// TW = 128/KW rows and a tile 8 TW rows (256 at KW = 4, 128 at KW = 8): 4x /
+// 2x the rows of a k_rows_ws tile, so a rank runs 2-4 units per CU instead
+// of 8.  The X image rows are the window only (32 / 64 B), up to WSN_UCAP
+// of them, addressed by u16 image offsets.  Per tile, rows sorted by
+// decreasing length are dealt TW at a time to the 8 compute waves (wave
+// groups g and 7 - g share a SIMD); a wave's rows run in lockstep batches of
+// 8 entries, its teams' batches interleaved (offsets of batch b of team k in
+// the 16-byte chunk base + b TW + k: 8 u16; value pair q of that batch in
+// chunk vbase + (4 b + q) TW + k), so one wave read of 16 B per lane touches
+// TW consecutive chunks.  A row's entries past its length in its last batch
+// are pads: the zero image row and value -0.0 (summed: +-0 changes nothing).
+// ---------------------------------------------------------------------------
+constexpr int WSN_LW = 8;        // loader waves (8 compute + 8 loader = 1024 lanes)
+constexpr int WSN_GWORDS = 1024 + 96;  // global record: union ids [0, 1024), then 6 x 16 header words
+constexpr int WSN_G_NOFF = 1024, WSN_G_TN = 1040, WSN_G_NU = 1056, WSN_G_VOFF = 1072, WSN_G_TNV = 1088;
+struct WsnGeom {
+    int kw;     // window columns (4 or 8)
+    int ucap;   // union rows (the image holds ucap + 1: the last is zero)
+    int ncap;   // padded entries per tile
+    constexpr int tl() const { return kw / 2; }        // lanes per team
+    constexpr int tw() const { return 128 / kw; }      // teams (rows) per wave
+    constexpr int rows() const { return 8 * tw(); }    // rows per tile
+    constexpr int xrow() const { return 8 * kw; }      // image row bytes
+    constexpr int lwords() const { return rows() + 16; }  // LDS record: rows | nbat << 24, then per wave lbase, vbase
+};
+constexpr WsnGeom WSN_K4{4, 1023, 4096};
+constexpr WsnGeom WSN_K8{8, 639, 3072};
+constexpr WsnGeom wsn_geom(int kw) { return kw == 4 ? WSN_K4 : WSN_K8; }
+
+struct WsnPlan {
+    WsnGeom geom = WSN_K4;
+    int ntiles = 0;
+    std::vector<int> grec;         // WSN_GWORDS per tile
+    std::vector<int> lrec;         // geom.lwords() per tile
+    std::vector<uint16_t> loff;    // per entry: image row (ucap: pad, the zero row)
+    std::vector<int> tsrc;         // per value entry: CSR index (-1: pad)
+    std::vector<int> direct;       // rows over a cap alone
+    int64_t union_rows = 0, tiled_nnz = 0, entries = 0, ventries = 0;
+    int xcd[9] = {};
+};
+// Tiles from analyse_tiles (caps.ucap / ncap / maxrows follow the geometry;
+// caps.part_* as for build_ws_plan), each laid out per wave; a tile whose
+// layout overflows ncap is split in two until it fits, a single row that
+// cannot fit becomes direct.  Verified by replaying the kernel's reads.
+bool build_wsn_plan(int m, int n, const int *row_ptr, const int *col_idx, int kw, WsnPlan &out, std::string *err,
+                    const TileCaps &caps);
+
+// ---------------------------------------------------------------------------
 // Plan of the opt-in MFMA tile kernel k_rows_mfma (SMFV_PLAN_MFMA; within
 // tolerance, not bit-identical).  Same clustered tiles (WS caps); each tile's
 // rows in groups of 16 (one wave each); per group the 16 x union part of A is

@@ -120,7 +120,7 @@ PLAN_ONE_WAVEFRONT, PLAN_SIMPLE_ROWS, PLAN_CS, PLAN_WS = 64, 128, 256, 512
 PLAN_WS_GEOM1, PLAN_WS_GEOM2, PLAN_WS_GEOM3 = 1024, 2048, 4096
 PLAN_LIVE_VALUES = 8192  # (r5) the tiled kernel reads the live CSR values (no snapshot, no bind)
 PLAN_STATS = 17  # SMFV_PLAN_STATS
-PLAN_KERNELS = {0: None, 1: "k_rows_ws", 2: "k_rows_mfma", 3: "k_spmv_chunks"}
+PLAN_KERNELS = {0: None, 1: "k_rows_ws", 2: "k_rows_mfma", 3: "k_spmv_chunks", 5: "k_rows_wsn"}
 
 
 class SpmmPlan:

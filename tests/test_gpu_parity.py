@@ -990,3 +990,39 @@ def test_live_values_full_size_and_contract(gpu):
         torch.cuda.synchronize()
         assert torch.equal(Yl.view(torch.int64), Ys.view(torch.int64))
         del g
+
+
+@pytest.mark.parametrize("K", [4, 8])
+def test_narrow_team_tiles(gpu, K):
+    """(r5) K = 4 / 8 windows take the narrow-team tiles (k_rows_wsn: K/2
+    lanes per row, 256 / 128-row tiles, window-only X image with u16
+    offsets): bit-identical to the reference's order, into a padded Y (the
+    padding stays NaN), with direct rows; and identical to the k_rows_ws
+    NARROW form (tiled_kernel="ws", the A/B); on both cop20k stand-ins at
+    full size."""
+    rng = np.random.default_rng(200 + K)
+    mats = [smfv.gen_fem27(9000, 14, 14, 0.83, K), smfv.gen_random_rows(7000, 6000, 16, 2.0, 1500, K),
+            smfv.cop20k_surrogate(), smfv.inputs.cop20k_irregular_surrogate()]
+    for A in mats:
+        X = rng.uniform(-1, 1, (A.numCols, 32))
+        dA = smfv.DeviceCSR(A, gpu)
+        dXf = torch.from_numpy(X).to(gpu)
+        f = 32 - K - 4
+        Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, np.ascontiguousarray(X[:, f:f + K]))
+        for tk in ("auto", "ws"):
+            plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles="force", tiled_kernel=tk)
+            st = plan.stats()
+            assert st["tiled"] and st["kernel"] == ("k_rows_wsn" if tk == "auto" else "k_rows_ws"), st
+            Yb = torch.full((A.numRows, K + 3), np.nan, dtype=torch.float64, device=gpu)
+            plan.run(dXf[:, f:f + K], Yb[:, :K])
+            torch.cuda.synchronize()
+            assert np.array_equal(bits(Yb[:, :K].cpu().numpy()), bits(Yref)), (A.numRows, tk, st)
+            assert torch.isnan(Yb[:, K:]).all()
+        # values changed: the snapshot re-binds (per-entry gather) and the sums follow
+        dA.values.mul_(0.25)
+        plan = smfv.SpmmPlan(smfv.Variant.COLUMNWISE, dA, K, tiles="force")
+        Yb = torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu)
+        plan.run(dXf[:, f:f + K], Yb)
+        torch.cuda.synchronize()
+        Y4 = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values * 0.25, np.ascontiguousarray(X[:, f:f + K]))
+        assert np.array_equal(bits(Yb.cpu().numpy()), bits(Y4))

@@ -623,3 +623,30 @@ def test_ws_kernels_register_budget(tmp_path):
         assert vgpr <= 512 // waves_per_simd and spill == 0, (name, vgpr, spill)
         seen += 1
     assert seen >= 24, seen
+
+
+def test_narrow_team_plan_on_host():
+    """(r5) The k_rows_wsn plan of a 4 / 8-column window (a ColumnWise rank's
+    panel) is built and verified on the host (its reads replayed): every row
+    once, in CSR order, pads on the zero image row; on the cop20k stand-in it
+    runs well under half the units of k_rows_ws's 2,011 tiles, and a row too
+    long for a tile becomes direct."""
+    ip = ctypes.POINTER(ctypes.c_int)
+
+    def wsn(A, kw, r0=0, r1=None):
+        out = (ctypes.c_double * 6)()
+        _lib.call("smfv_wsn_plan_analyse", r0, A.numRows if r1 is None else r1, A.numCols,
+                  A.rowPtr.ctypes.data_as(ip), A.colIndices.ctypes.data_as(ip), kw, out)
+        return [float(v) for v in out]
+    A = smfv.inputs.cop20k_surrogate()
+    for kw, rows in ((4, 256), (8, 128)):
+        tiles, union, reuse, direct, most, entries = wsn(A, kw)
+        assert 0 < tiles < 2011 * 0.6 and direct == 0 and most <= rows and reuse > 6.0, (kw, tiles, reuse)
+        assert entries >= A.nnz
+    P = smfv.gen_random_rows(5000, 5000, 12, 2.0, 5000, 3)  # a few very long rows
+    tiles, union, reuse, direct, most, entries = wsn(P, 4)
+    assert tiles > 0 and direct >= 1
+    tiles_b, *_ = wsn(A, 8, 30000, 90000)  # a row block (columns shifted by its first row)
+    assert tiles_b > 0
+    with pytest.raises(RuntimeError):
+        wsn(A, 16)
