@@ -1109,6 +1109,8 @@ def main() -> None:
                          "per CU (SMFV_PLAN_WS_GEOM1 / 2 / 3)")
     ap.add_argument("--live-values", action="store_true",
                     help="tiled plans read the live CSR values (SMFV_PLAN_LIVE_VALUES: no snapshot, bind a no-op)")
+    ap.add_argument("--single-rows", action="store_true",
+                    help="one row per k_rows_ws team: no row pairs (SMFV_PLAN_SINGLE_ROWS, A/B)")
     ap.add_argument("--fma", action="store_true",
                     help="time the opt-in FMA plans (SMFV_PLAN_FMA) instead of the bit-exact ones")
     ap.add_argument("--rank-plans", type=int, default=0,
@@ -1211,7 +1213,8 @@ def main() -> None:
         t0 = time.time()
         plan = smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles, fma=args.fma, seeds=args.seeds,
                              mfma=args.mfma, split_ends=args.split_ends, xcd_parts=args.xcd_parts,
-                             tiled_kernel=args.tiled_kernel, live_values=args.live_values)
+                             tiled_kernel=args.tiled_kernel, live_values=args.live_values,
+                             single_rows=args.single_rows)
         torch.cuda.synchronize()
         t_plan.append(time.time() - t0)
         copies.append((plan, dX, dY))
@@ -1395,7 +1398,7 @@ def main() -> None:
                          "size_matched_copy": (dict(copy_floor, frac_of_copy_time=round(copy_floor["avg_launch_ms"] / kern_ms, 4))
                                                if copy_floor else None)},
             "plan": {"tiled": st["tiled"], "tiles": st["tiles"], "reuse": round(st["reuse"], 3),
-                     "live_values": st["live_values"],
+                     "live_values": st["live_values"], "paired_rows": st.get("paired_rows"),
                      "est_reuse_sampled": round(st["est_reuse"], 3), "direct_rows": st["direct_rows"],
                      "create_s": round(t_plan[0], 3), "analysis_ms": round(st["analysis_ms"], 1),
                      "bind_ms": round(bind_ms, 4), "snapshot_entries": st["snapshot_entries"],

@@ -212,6 +212,14 @@ typedef struct smfv_plan_s *smfv_plan_t;
  * plan).  Bit-identical to the snapshot path.  Tiled k_rows_ws plans only
  * (K = 1 chunk plans and SMFV_PLAN_MFMA keep their snapshot). */
 #define SMFV_PLAN_LIVE_VALUES 8192
+/* (r5) Without this flag a k_rows_ws tile may hold up to twice its teams in
+ * rows: the shortest rows ride as second rows of the teams of the next
+ * shortest (a team sums its first row, stores it, then sums its second), so
+ * the tiles of short-row patterns stop at the X-row and entry caps instead of
+ * the row count.  Same per-row order: bit-identical.  Snapshot plans only
+ * (live-values plans keep one row per team).  This flag keeps one row per
+ * team (A/B). */
+#define SMFV_PLAN_SINGLE_ROWS 16384
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
 /* Plan of the row block [row_begin, row_end) of a CSR matrix (h_row_ptr /
@@ -277,8 +285,9 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
  * geometry (1: one 1024-lane block per CU, 2: two 512-lane blocks, 3: one
  * 768-lane block; 0 other); [16] (r4) 1 if a bind writes the snapshot's real
  * entries from bind items of up to 4 consecutive non-zeros (pads written once
- * at create: k_bind_items), 0 if it gathers every entry by index */
-#define SMFV_PLAN_STATS 17
+ * at create: k_bind_items), 0 if it gathers every entry by index; [17] (r5)
+ * rows summed as a team's second row (SMFV_PLAN_SINGLE_ROWS) */
+#define SMFV_PLAN_STATS 18
 SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS]);
 SMFV_API int smfv_plan_destroy(smfv_plan_t plan);
 

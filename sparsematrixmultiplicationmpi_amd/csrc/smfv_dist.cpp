@@ -897,11 +897,11 @@ SMFV_API int smfv_dist_plan_stats(smfv_dist_plan_t d, double out[SMFV_PLAN_STATS
             if (rc) return rc;
             if (first) {
                 for (int i = 0; i < SMFV_PLAN_STATS; ++i) out[i] = o[i];
-                for (int i : {1, 2, 4, 5, 8, 9}) out[i] = 0.0;
+                for (int i : {1, 2, 4, 5, 8, 9, 17}) out[i] = 0.0;
                 first = false;
             }
             out[0] = out[0] && o[0];
-            for (int i : {1, 2, 4, 5, 8, 9}) out[i] += o[i];
+            for (int i : {1, 2, 4, 5, 8, 9, 17}) out[i] += o[i];
             reuse_w += o[3] * o[2];
         }
         out[3] = out[2] > 0 ? reuse_w / out[2] : 0.0;

@@ -579,13 +579,13 @@ __device__ __forceinline__ bufrsrc make_rsrc(const void *base, unsigned bytes)
 // (r4) LDS layout of a k_rows_ws geometry (WsGeom, smfv_plan.h): two X
 // images of UCAP + 1 rows (the last one zero), then two meta slots of values,
 // u8 offsets and the tile's record ([0, R) rows, [R, 2R) L bases, [2R, 3R) V
-// bases; 1 KiB for 64-row tiles, 384 B rounded to 512 for 32-row tiles)
+// bases, (r5) [3R, 4R) second rows; 1 KiB for 64-team tiles, 512 B for 32)
 template <int CW, int LW, int PPW, int UCAP, int NCAP> struct Lay {
     static constexpr int R = 8 * CW;
     static constexpr int XSLOT = (UCAP + 1) * 256;
     static constexpr int SL_M = 2 * XSLOT;
     static constexpr int M_V = 0, M_L = (NCAP + 127) / 128 * 1024, M_R = M_L + (NCAP + 1023) / 1024 * 1024;
-    static constexpr int REC_LANES = CW == 8 ? 64 : 3 * R / 4;  // 16 B per lane
+    static constexpr int REC_LANES = CW == 8 ? 64 : R;  // 16 B per lane (4 words per team slot)
     static constexpr int RECB = CW == 8 ? 1024 : (REC_LANES * 16 + 255) / 256 * 256;
     static constexpr int MSLOT = M_R + RECB;
     static constexpr int BYTES = SL_M + 2 * MSLOT;
@@ -796,15 +796,18 @@ __device__ __forceinline__ void ws_body(int xfirst, int xend, int npanel, int ch
         const char *xbase = lds + (u & 1) * XSLOT;
         const char *mbase = lds + SL_M + (it & 1) * MSLOT;
         const int *R = reinterpret_cast<const int *>(mbase + M_R);
-        const int row = R[slot];
-        if (row >= 0) {
-            const int info = R[L::R + slot];
+        int row = R[slot];
+        // (r5) a team may sum a second row after its first (row pairs: the
+        // record's [3R, 4R), -1 none; its entries start at the batch after the
+        // first row's last); snapshot plans only
+        const int pw = LIVE ? -1 : R[3 * L::R + slot];
+        int info = R[L::R + slot], vw = R[2 * L::R + slot];
+        for (; row >= 0;) {
             // the row runs nbat whole batches of 8, then rem (0, 2, 4 or 6)
             // entries of one more (its length rounded up to even)
             const int js = info & 0xFFFF, len = info >> 16, nbat = len >> 3, rem = len & 7;
             const int blast = nbat + (rem ? 1 : 0) - 1;
             const u2 *Lq = reinterpret_cast<const u2 *>(mbase + M_L) + js + qk;
-            const int vw = R[2 * L::R + slot];
             // (the LIVE flag bits sit above bit 16: a snapshot plan's word is the base itself)
             const d2 *Vq = reinterpret_cast<const d2 *>(mbase + M_V) + (LIVE ? (vw & 0xFFFF) : vw) + qk;
             if constexpr (LIVE)
@@ -926,6 +929,13 @@ __device__ __forceinline__ void ws_body(int xfirst, int xend, int npanel, int ch
                 __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y + 16 * par));
                 __builtin_nontemporal_store(acc1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
             }
+            if (LIVE || pw < 0 || row == (pw & 0xFFFFFF)) break;
+            // the second row: from the batch after the first row's last (an
+            // empty first row owns one batch)
+            const int nb = max(1, (len + 7) >> 3);
+            row = pw & 0xFFFFFF;
+            info = (js + 4 * nb) | ((pw >> 24) << 16);
+            vw += 16 * nb;
         }
         if (++p == npanel) p = 0, ++it;
         barrier_lds();  // X slot (u & 1) is free for unit u + 2, meta slot for tile it + 1
@@ -1998,6 +2008,7 @@ static TileCaps plan_caps(int flags, int col_base)
     caps.frontier = !(flags & SMFV_PLAN_NATURAL_SEEDS);
     caps.split_ends = (flags & SMFV_PLAN_SPLIT_ENDS) ? SMFV_WS_BLOCKS_PER_XCD : 0;
     caps.col_base = col_base;  // a row block's neighbours are its columns shifted by its first global row
+    caps.pairs = !(flags & SMFV_PLAN_SINGLE_ROWS);
     return caps;
 }
 
@@ -2039,6 +2050,7 @@ struct smfv_plan_s {
     double reuse = 0.0, est_reuse = -1.0, analysis_ms = 0.0;
     int ws_xcd[9] = {};            // XCD x runs tiles [ws_xcd[x], ws_xcd[x + 1])
     int ws_geom = 0;               // (r4) k_rows_ws geometry: WsGeom::id (1, 2, 3)
+    int64_t paired = 0;            // (r5) rows summed as a team's second row
     int parts = 1;                 // 8: one part of the rows per XCD (build_ws_plan)
     double footprint = -1.0;       // parts_footprint of the 8 parts
     int *tsrc = nullptr;                   // snapshot entry -> CSR index of its value (-1: pad); NULL with descriptors
@@ -2357,6 +2369,7 @@ int smfv::plan_create(smfv_plan_t *out, int variant, int row_begin, int m, int n
             if (built) {
                 p->ws_geom = W.geom.id;
                 p->ntiles = W.ntiles;
+                p->paired = W.paired;
                 for (int x = 0; x <= 8; ++x) p->ws_xcd[x] = W.xcd[x];
                 p->parts = caps.part_start.size() > 2 ? (int)caps.part_start.size() - 1 : 1;
                 p->union_rows = W.union_rows;
@@ -2741,6 +2754,7 @@ SMFV_API int smfv_plan_stats(smfv_plan_t plan, double out[SMFV_PLAN_STATS])
     out[14] = plan->live ? 1.0 : 0.0;  // (r5) live values (k_rows_cs, which used this slot, is retired)
     out[15] = plan->tiled && !plan->k1 && !plan->mfma && !plan->wsn ? plan->ws_geom : 0;
     out[16] = plan->bind_desc ? 1.0 : 0.0;
+    out[17] = (double)plan->paired;
     return SMFV_OK;
 }
 

@@ -380,10 +380,17 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
             (int64_t)voff + tnv > P.ventries)
             return fail("tile header out of range");
         for (int slot = 0; slot < R; ++slot) {
-            const int r = l[slot];
-            if (r == -1) continue;
+            const int r = l[slot], pw = l[3 * R + slot];
+            if (r == -1) {
+                if (pw != -1) return fail("second row in an empty team");
+                continue;
+            }
             if (r < 0 || r >= m || seen[r]) return fail("tile row out of range or repeated");
             seen[r] = 1;
+            if (pw == -1) continue;
+            const int r2 = pw & 0xFFFFFF;
+            if (P.live || pw < 0 || r2 >= m || seen[r2]) return fail("second row out of range or repeated");
+            seen[r2] = 1;
         }
     }
     for (int r = 0; r < m; ++r)
@@ -401,14 +408,10 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
         for (int e = noff; e < noff + tn; ++e)
             if (P.loff[e] != G.ucap && P.loff[e] >= nu)
                 return "entry offset outside the tile's union";
-        for (int slot = 0; slot < R; ++slot) {
-            const int r = l[slot];
-            if (r == -1) continue;
-            const int lb = l[R + slot] & 0xFFFF, len = l[R + slot] >> 16, vb = l[2 * R + slot] & 0xFFFF;
-            const int k = (slot / G.cw) & 3;  // the team's position in its quad
+        // one row of a team: L base lb, V base vb, summed length len
+        auto check_row = [&](int r, int lb, int len, int vb, int k) -> const char * {
             const int rl = rp[r + 1] - rp[r];
             if (len % 2 || len < rl || len > rl + 1) return "row segment length";
-            if ((l[2 * R + slot] & ~0xFFFF) != (P.live && rl % 2 ? 1 << 30 : 0)) return "row value flags";
             if (P.live)  // each value slot the row sums starts at its pair of CSR values
                 for (int c = 0; c < len / 2; ++c) {
                     const int64_t s = (int64_t)t * P.vstride + vb + 4 * c + k;
@@ -440,6 +443,23 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
                         return "pad entry does not read the zero row";
                     }
                 }
+            return nullptr;
+        };
+        for (int slot = 0; slot < R; ++slot) {
+            const int r = l[slot];
+            if (r == -1) continue;
+            const int lb = l[R + slot] & 0xFFFF, len = l[R + slot] >> 16, vb = l[2 * R + slot] & 0xFFFF;
+            const int k = (slot / G.cw) & 3;  // the team's position in its quad
+            const int rl = rp[r + 1] - rp[r];
+            if ((l[2 * R + slot] & ~0xFFFF) != (P.live && rl % 2 ? 1 << 30 : 0)) return "row value flags";
+            if (const char *e = check_row(r, lb, len, vb, k)) return e;
+            const int pw = l[3 * R + slot];
+            if (pw != -1) {
+                // the second row starts at the batch after the first row's
+                // last (an empty first row still owns one batch)
+                const int nb = std::max(1, (len + 7) / 8);
+                if (const char *e = check_row(pw & 0xFFFFFF, lb + 4 * nb, pw >> 24, vb + 16 * nb, k)) return e;
+            }
         }
         return nullptr;
     };
@@ -543,8 +563,17 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         if (err) *err = "ws plan: unsupported geometry";
         return false;
     }
+    // (r5) row pairs: a tile may hold up to twice the kernel's teams in rows;
+    // the rows past one per team go, shortest first, as second rows to the
+    // teams of the next-shortest (the row index and its even length share
+    // one record word: < 2^24 rows, second rows of <= 126 entries)
+    const bool pairs = caps.pairs && !caps.live && m < (1 << 24);
     TileAnalysis T;
-    analyse_tiles(m, n, rp, ci, T, caps);  // caps.ucap / ncap / maxrows follow caps.geom (plan_caps)
+    {
+        TileCaps ac = caps;  // ucap / ncap / maxrows follow caps.geom (plan_caps)
+        if (pairs) ac.maxrows = 2 * G.rows();
+        analyse_tiles(m, n, rp, ci, T, ac);
+    }
     tick("analyse_tiles");
 
     auto len8 = [&](int r) { return std::max(8, (rp[r + 1] - rp[r] + 7) & ~7); };
@@ -552,20 +581,62 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     // ends a row on 0, 2, 4 or 6 entries of a last batch); its storage stays
     // whole batches (quad layout, len8)
     auto len2 = [&](int r) { return (rp[r + 1] - rp[r] + 1) & ~1; };
-    // entries of a row set sorted by decreasing length: a quad takes 4x its first (longest) row
+    // a team (its first row r): second row, whole-batch and summed lengths --
+    // the second row's entries follow the first's last batch
+    std::vector<int> partner(pairs ? (size_t)m : 0, -1);
+    auto second = [&](int r) { return pairs ? partner[(size_t)r] : -1; };
+    auto tlen8 = [&](int r) {
+        const int b = second(r);
+        return len8(r) + (b >= 0 ? len8(b) : 0);
+    };
+    auto tlen2 = [&](int r) {
+        const int b = second(r);
+        return b >= 0 ? len8(r) + len2(b) : len2(r);
+    };
+    // a tile's rows -> its teams (first rows, by decreasing length); false if
+    // the rows cannot be teamed (too many, or a second row too long)
+    auto make_teams = [&](std::vector<int> &R) -> bool {
+        const int NR = G.rows();
+        if ((int)R.size() > (pairs ? 2 * NR : NR)) return false;
+        std::sort(R.begin(), R.end(), [&](int a, int b) {
+            const int la = rp[a + 1] - rp[a], lb = rp[b + 1] - rp[b];
+            return la != lb ? la > lb : a < b;
+        });
+        if (!pairs) return true;
+        for (int r : R) partner[(size_t)r] = -1;
+        if ((int)R.size() > NR) {
+            // the 2 np shortest rows in np teams, the i-th longest with the
+            // i-th shortest (even team lengths)
+            const size_t n = R.size(), np = n - (size_t)NR, b = n - 2 * np;
+            for (size_t i = 0; i < np; ++i)
+                if (len2(R[n - 1 - i]) > 126) return false;
+            for (size_t i = 0; i < np; ++i) partner[(size_t)R[b + i]] = R[n - 1 - i];
+            R.resize(n - np);
+            std::sort(R.begin(), R.end(), [&](int a, int b) {
+                const int la = tlen8(a), lb = tlen8(b), sa = tlen2(a), sb = tlen2(b);
+                return la != lb ? la > lb : sa != sb ? sa > sb : a < b;
+            });
+        }
+        return true;
+    };
+    // entries of a team set sorted by decreasing length: a quad takes 4x its first (longest) team
     auto layout = [&](const std::vector<int> &rows) {
         int64_t e = 0;
-        for (size_t q = 0; q < rows.size(); q += 4) e += 4 * (int64_t)len8(rows[q]);
+        for (size_t q = 0; q < rows.size(); q += 4) e += 4 * (int64_t)tlen8(rows[q]);
         return e;
+    };
+    auto fits = [&](const std::vector<int> &R) {
+        std::vector<int> h = R;
+        return make_teams(h) && layout(h) <= G.ncap;
     };
     // value entries of a quad: its offsets' 32 per batch, less the value
     // pairs of its last batch that no row sums (pair groups q >= qmax of a
     // batch sit last in the quad's value range: rows of 27 store 28, not 32)
     auto vquad = [&](const std::vector<int> &rows, size_t q0) {
-        const int nb = len8(rows[q0]) / 8;
+        const int nb = tlen8(rows[q0]) / 8;
         int qmax = 0;
         for (size_t k = q0; k < q0 + 4 && k < rows.size(); ++k)
-            if (len8(rows[k]) / 8 == nb) qmax = std::max(qmax, (len2(rows[k]) - 8 * (nb - 1) + 1) / 2);
+            if (tlen8(rows[k]) / 8 == nb) qmax = std::max(qmax, (tlen2(rows[k]) - 8 * (nb - 1) + 1) / 2);
         return 32 * (int64_t)nb - 8 * (int64_t)(4 - qmax);
     };
     auto vlayout = [&](const std::vector<int> &rows) {
@@ -579,12 +650,13 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     auto emit = [&](const std::vector<int> &R, int64_t noff, int64_t vnoff, int t, std::vector<int> &pos,
                     std::vector<int> &stamp, std::vector<int> &ucols, int64_t &tiled, int64_t &unions) {
         ucols.clear();
-        for (int r : R)
-            for (int j = rp[r]; j < rp[r + 1]; ++j)
-                if (pos[ci[j]] < 0) {
-                    pos[ci[j]] = (int)ucols.size();
-                    ucols.push_back(ci[j]);
-                }
+        for (int r0 : R)
+            for (int r = r0; r >= 0; r = r == r0 ? second(r0) : -1)
+                for (int j = rp[r]; j < rp[r + 1]; ++j)
+                    if (pos[ci[j]] < 0) {
+                        pos[ci[j]] = (int)ucols.size();
+                        ucols.push_back(ci[j]);
+                    }
         const int nu = (int)ucols.size();
         // issue order: loader wave w stages pieces w, w + 8, ... (4 union
         // rows each) in that order, so positions go out in ascending order;
@@ -606,7 +678,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         int *lrec = &P.lrec[(size_t)t * WS_LWORDS];
         int *grec = &P.grec[(size_t)t * WS_GWORDS];
         const int NR = G.rows();
-        for (int s = 0; s < NR; ++s) lrec[s] = -1;
+        for (int s = 0; s < NR; ++s) lrec[s] = lrec[3 * NR + s] = -1;
         int64_t e = 0, ev = 0;
         for (int q = 0; 4 * q < (int)R.size(); ++q) {
             // 8 compute waves: octet o = quads 2o, 2o + 1 -> one wave, and SIMD s
@@ -615,23 +687,30 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
             // q / 4, so a tile of fewer than 32 rows still keeps all 4 waves busy
             const int o = q / 2;
             const int w = G.cw == 8 ? (o < 4 ? o : 11 - o) : q % 4, h = G.cw == 8 ? q % 2 : q / 4;
-            const int nb = len8(R[4 * q]) / 8;
+            const int nb = tlen8(R[4 * q]) / 8;
             const int lbase = (int)(e / 8), vbase = (int)(ev / 2);
             for (int k = 0; k < 4 && 4 * q + k < (int)R.size(); ++k) {
-                const int r = R[4 * q + k], slot = (4 * h + k) * G.cw + w;
-                for (int j = rp[r]; j < rp[r + 1]; ++j) {
-                    const int el = j - rp[r];
-                    P.loff[(size_t)(noff + (int64_t)(lbase + 4 * (el / 8) + k) * 8 + el % 8)] =
-                        (uint8_t)pos[ci[j]];
-                    if (!P.live) P.tsrc[(size_t)(vnoff + (int64_t)(vbase + 4 * (el / 2) + k) * 2 + el % 2)] = j;
-                }
+                const int r = R[4 * q + k], slot = (4 * h + k) * G.cw + w, r2 = second(r);
+                // the team's entries: its first row's, then (from the batch
+                // after the first row's last) its second row's
+                for (int r1 = r, e0 = 0; r1 >= 0; e0 = len8(r), r1 = r1 == r ? r2 : -1)
+                    for (int j = rp[r1]; j < rp[r1 + 1]; ++j) {
+                        const int el = e0 + j - rp[r1];
+                        P.loff[(size_t)(noff + (int64_t)(lbase + 4 * (el / 8) + k) * 8 + el % 8)] =
+                            (uint8_t)pos[ci[j]];
+                        if (!P.live) P.tsrc[(size_t)(vnoff + (int64_t)(vbase + 4 * (el / 2) + k) * 2 + el % 2)] = j;
+                    }
                 const int rl = rp[r + 1] - rp[r];
                 if (P.live)  // (r5) value slot of pair c: its first entry's CSR index
                     for (int c = 0; c < len2(r) / 2; ++c) P.vidx[(size_t)t * P.vstride + vbase + 4 * c + k] = rp[r] + 2 * c;
                 lrec[slot] = r;
                 lrec[NR + slot] = lbase | (len2(r) << 16);
                 lrec[2 * NR + slot] = vbase | (P.live && rl % 2 ? 1 << 30 : 0);
-                tiled += rp[r + 1] - rp[r];
+                tiled += rl;
+                if (r2 >= 0) {
+                    lrec[3 * NR + slot] = r2 | (len2(r2) << 24);
+                    tiled += rp[r2 + 1] - rp[r2];
+                }
             }
             e += 32 * nb;
             ev += vquad(R, (size_t)(4 * q));
@@ -671,17 +750,18 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
             P.direct.insert(P.direct.end(), rows.begin(), rows.end());
             continue;
         }
-        std::vector<int> sorted = rows;
-        by_length(sorted);
-        if (layout(sorted) <= G.ncap) {
+        if (fits(rows)) {
             tiles.push_back(std::move(rows));
             continue;
         }
+        ++P.split;
+        std::vector<int> sorted = rows;
+        by_length(sorted);
         stack.assign(1, sorted);
         while (!stack.empty()) {
             std::vector<int> R = std::move(stack.back());
             stack.pop_back();
-            if (layout(R) <= G.ncap) {
+            if (fits(R)) {
                 tiles.push_back(std::move(R));
             } else if (R.size() == 1) {
                 P.direct.push_back(R[0]);
@@ -742,9 +822,15 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     const int nt = (int)tiles.size();
     std::vector<int64_t> toff((size_t)nt + 1, 0), tvoff((size_t)nt + 1, 0);
     for (int t = 0; t < nt; ++t) {
-        by_length(tiles[(size_t)t]);
-        toff[(size_t)t + 1] = toff[(size_t)t] + layout(tiles[(size_t)t]);
-        tvoff[(size_t)t + 1] = tvoff[(size_t)t] + vlayout(tiles[(size_t)t]);
+        std::vector<int> &R = tiles[(size_t)t];
+        const size_t rows = R.size();
+        if (!make_teams(R)) {  // (a half of split_ends: fewer rows than a tile that fit)
+            if (err) *err = "ws plan: a tile's rows do not form teams";
+            return false;
+        }
+        P.paired += (int64_t)(rows - R.size());
+        toff[(size_t)t + 1] = toff[(size_t)t] + layout(R);
+        tvoff[(size_t)t + 1] = tvoff[(size_t)t] + vlayout(R);
     }
     P.ntiles = nt;
     P.entries = toff[(size_t)nt];
@@ -768,9 +854,10 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
         auto unite = [&](int w) {
             std::vector<int> seen((size_t)std::max(n, 1), -1);
             for (int t = (int)((int64_t)nt * w / nth); t < (int)((int64_t)nt * (w + 1) / nth); ++t)
-                for (int r : tiles[(size_t)t])
-                    for (int j = rp[r]; j < rp[r + 1]; ++j)
-                        if (seen[ci[j]] != t) seen[ci[j]] = t, tunion[(size_t)t].push_back(ci[j]);
+                for (int r0 : tiles[(size_t)t])
+                    for (int r = r0; r >= 0; r = r == r0 ? second(r0) : -1)
+                        for (int j = rp[r]; j < rp[r + 1]; ++j)
+                            if (seen[ci[j]] != t) seen[ci[j]] = t, tunion[(size_t)t].push_back(ci[j]);
         };
         auto work = [&](int w) {
             std::vector<int> pos((size_t)std::max(n, 1), -1), stamp((size_t)std::max(n, 1), -1), ucols;

@@ -42,7 +42,9 @@ constexpr int WS_GWORDS = 352, WS_G_NOFF = 256, WS_G_TN = 272, WS_G_NU = 288, WS
 // LDS record (per tile, 256 int32 = 1 KiB in global memory): with R rows per
 // tile, [0, R) row per team slot (-1 none), [R, 2R) L chunk base | (padded
 // length << 16), [2R, 3R) V chunk base; team slot = team-in-wave * (compute
-// waves) + wave
+// waves) + wave; (r5) [3R, 4R) the team's second row | its length (rounded
+// up to even) << 24, or -1: the team sums it after the first, from the batch
+// after the first row's last (TileCaps::pairs)
 constexpr int WS_LWORDS = 256;
 constexpr int WS_SLACK = 2048;   // entries past the end (DMA over-read of the last tile)
 
@@ -125,6 +127,9 @@ struct TileCaps {
     int xcd_blocks = 32;           // k_rows_ws blocks per XCD (MI355X: 256 CUs / 8 XCDs)
     WsGeom geom = WS_GEOM1;        // build_ws_plan: the kernel geometry (ucap / ncap / maxrows follow it)
     bool live = false;             // build_ws_plan: live values (WsPlan::vidx) instead of a snapshot (tsrc)
+    // (r5) build_ws_plan: tiles of up to 2 x geom.rows() rows, a team summing
+    // two short rows one after the other (snapshot plans of < 2^24 rows)
+    bool pairs = false;
 };
 // Independent parts are analysed on up to 8 threads; analysis_threads > 0
 // caps that for analyses run on the calling thread (smfv_set_analysis_threads).
@@ -158,6 +163,8 @@ struct WsPlan {
     int64_t ventries = 0;          // used length of tsrc (the vector carries WS_SLACK more): a quad's
                                    // last batch stores only the value pairs its rows use
     int xcd[9] = {};               // XCD x runs tiles [xcd[x], xcd[x + 1])
+    int64_t paired = 0;            // (r5) second rows of teams (TileCaps::pairs)
+    int64_t split = 0;             // analysed tiles whose layout had to be split
 };
 
 // Tiles from analyse_tiles (WS caps), each packed into the interleaved

@@ -119,7 +119,8 @@ PLAN_NO_TILES, PLAN_FORCE_TILES, PLAN_FMA, PLAN_NATURAL_SEEDS, PLAN_MFMA, PLAN_S
 PLAN_ONE_WAVEFRONT, PLAN_SIMPLE_ROWS, PLAN_CS, PLAN_WS = 64, 128, 256, 512
 PLAN_WS_GEOM1, PLAN_WS_GEOM2, PLAN_WS_GEOM3 = 1024, 2048, 4096
 PLAN_LIVE_VALUES = 8192  # (r5) the tiled kernel reads the live CSR values (no snapshot, no bind)
-PLAN_STATS = 17  # SMFV_PLAN_STATS
+PLAN_SINGLE_ROWS = 16384  # (r5) one row per k_rows_ws team (no row pairs; A/B)
+PLAN_STATS = 18  # SMFV_PLAN_STATS
 PLAN_KERNELS = {0: None, 1: "k_rows_ws", 2: "k_rows_mfma", 3: "k_spmv_chunks", 5: "k_rows_wsn"}
 
 
@@ -141,12 +142,15 @@ class SpmmPlan:
     def __init__(self, variant: int, A: DeviceCSR, K: int, tiles: str = "auto", fma: bool = False,
                  stream: torch.cuda.Stream | None = None, rows: tuple[int, int] | None = None,
                  seeds: str = "frontier", mfma: bool = False, split_ends: bool = False,
-                 xcd_parts: str = "auto", tiled_kernel: str = "auto", live_values: bool = False):
+                 xcd_parts: str = "auto", tiled_kernel: str = "auto", live_values: bool = False,
+                 single_rows: bool = False):
         self.variant, self.A, self.K = Variant(variant), A, K
         self.rows = rows
         flags = {"auto": 0, "off": PLAN_NO_TILES, "force": PLAN_FORCE_TILES}[tiles]
         if live_values:  # (r5) SMFV_PLAN_LIVE_VALUES: value pairs DMA'd from the CSR values, bind a no-op
             flags |= PLAN_LIVE_VALUES
+        if single_rows:  # (r5) one row per k_rows_ws team, no row pairs (SMFV_PLAN_SINGLE_ROWS, A/B)
+            flags |= PLAN_SINGLE_ROWS
         if fma:  # opt-in fused multiply-add in the tiled kernel: within tolerance, not bit-identical
             flags |= PLAN_FMA
         if seeds == "natural":  # tiles seeded in row order (A/B of the wavefront seeding)
@@ -189,7 +193,8 @@ class SpmmPlan:
                 "row_begin": int(out[6]), "est_reuse": float(out[7]), "analysis_ms": float(out[8]),
                 "snapshot_entries": int(out[9]), "mfma": bool(out[10]), "xcd_parts": int(out[11]),
                 "footprint": float(out[12]), "kernel": PLAN_KERNELS.get(int(out[13])), "live_values": bool(out[14]),
-                "ws_geom": int(out[15]), "bind_descriptors": bool(out[16])}
+                "ws_geom": int(out[15]), "bind_descriptors": bool(out[16]),
+                "paired_rows": int(out[17])}
 
     def run(self, X: torch.Tensor, Y: torch.Tensor, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
         A, K = self.A, self.K

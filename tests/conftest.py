@@ -77,3 +77,26 @@ def gpu():
         pytest.skip("no GPU")
     torch.cuda.set_device(0)
     return torch.device("cuda", 0)
+
+
+def short_rows_band(m, seed, long_every=97):
+    """(r5) A pattern for row-pair tiles: rows of 0-7 non-zeros (every
+    residue, empty rows included) from a +-12 band, every `long_every`-th row
+    30-60 long -- tiles stop at their row count, so the shortest rows ride as
+    second rows of teams.  Values uniform in [-1, 1)."""
+    import numpy as np
+    from sparsematrixmultiplicationmpi_amd import inputs
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 8, m)
+    lens[::long_every] = rng.integers(30, 61, lens[::long_every].size)
+    cols = []
+    for i, L in enumerate(lens):
+        lo, hi = max(0, i - 12), min(m, i + 13)
+        if L > hi - lo:
+            lo, hi = max(0, i - 40), min(m, i + 41)
+            L = lens[i] = min(L, hi - lo)
+        cols.append(np.sort(rng.choice(np.arange(lo, hi), int(L), replace=False)))
+    rp = np.zeros(m + 1, np.int32)
+    rp[1:] = np.cumsum(lens)
+    ci = np.concatenate(cols).astype(np.int32)
+    return inputs.SparseMatrix(rng.uniform(-1, 1, ci.size), ci, rp, m, m)

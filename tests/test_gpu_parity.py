@@ -1026,3 +1026,48 @@ def test_narrow_team_tiles(gpu, K):
         torch.cuda.synchronize()
         Y4 = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values * 0.25, np.ascontiguousarray(X[:, f:f + K]))
         assert np.array_equal(bits(Yb.cpu().numpy()), bits(Y4))
+
+
+@pytest.mark.parametrize("tk", ["auto", "ws2", "ws3"])
+def test_row_pair_tiles(gpu, tk):
+    """(r5) Row pairs: teams summing a second (short) row after their first
+    (the default; SMFV_PLAN_SINGLE_ROWS keeps one row per team) -- on a
+    0-7-entry band with long rows (every residue, empty rows), a row block
+    starting mid-matrix and the irregular cop20k_A stand-in; K = 32 / 64 /
+    128 and a 16-column window of a wider X (NARROW): bit-identical to the
+    reference's order and to the single-row plan, and after a value change
+    (the bind items re-gather the paired rows' values)."""
+    from conftest import short_rows_band
+    rng = np.random.default_rng(300)
+    mats = [short_rows_band(20000, 3)] + ([smfv.inputs.cop20k_irregular_surrogate()] if tk == "auto" else [])
+    for A in mats:
+        dA = smfv.DeviceCSR(A, gpu)
+        X = rng.uniform(-1, 1, (A.numCols, 128))
+        dXf = torch.from_numpy(X).to(gpu)
+        for K, f, rows in ((32, 0, None), (64, 32, None), (128, 0, None), (16, 8, None), (32, 0, (777, 15000))):
+            Xw = np.ascontiguousarray(X[:, f:f + K])
+            r0, r1 = rows or (0, A.numRows)
+            Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, Xw)[r0:r1]
+            outs = []
+            for single in (False, True):
+                plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles="force", rows=rows, single_rows=single,
+                                     tiled_kernel="auto" if tk == "auto" else tk)
+                st = plan.stats()
+                assert st["tiled"] and st["kernel"] == "k_rows_ws", st
+                assert (st["paired_rows"] > 0) != single, st
+                Yb = torch.full((r1 - r0, K + 1), np.nan, dtype=torch.float64, device=gpu)
+                plan.run(dXf[:, f:f + K], Yb[:, :K])
+                torch.cuda.synchronize()
+                outs.append(Yb[:, :K].cpu().numpy())
+                assert np.array_equal(bits(outs[-1]), bits(Yref)), (K, f, rows, single, st)
+                assert torch.isnan(Yb[:, K:]).all()
+        # values changed: a re-bind gathers the paired rows' values too
+        dA.values.mul_(-0.5)
+        plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, 32, tiles="force")
+        dA.values.mul_(-2.0)
+        plan.bind_values()
+        Y = torch.full((A.numRows, 32), np.nan, dtype=torch.float64, device=gpu)
+        plan.run(dXf[:, :32], Y)
+        torch.cuda.synchronize()
+        Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, np.ascontiguousarray(X[:, :32]))
+        assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref)), plan.stats()

@@ -251,13 +251,42 @@ def test_ws_geometry2_plans_verify():
     A = smfv.cop20k_surrogate()
     g1, g2 = _analyse_rows(A, 0, A.numRows, G1), _analyse_rows(A, 0, A.numRows, G2)
     assert g1 == _analyse_rows(A, 0, A.numRows)  # the default is geometry 1
-    assert g1["tiles"] == 2011 and g2["direct"] == 0
+    # (r5) 2011 tiles of one row per team; 1960 with row pairs (the default)
+    assert _analyse_rows(A, 0, A.numRows, G1 | SINGLE_ROWS)["tiles"] == 2011
+    assert g1["tiles"] == 1960 and g2["direct"] == 0
     assert 2.4 * g1["tiles"] < g2["tiles"] < 2.7 * g1["tiles"] and g2["reuse"] > 4.0
     for name in ("empty7x5.mtx", "pat4x6.mtx"):
         B = smfv.readMatrixMarketFile(os.path.join(GOLDEN, name))
         assert _analyse_rows(B, 0, B.numRows, G2)["tiles"] >= 1, name
     # a row block starting mid-matrix (a rank's share)
     assert _analyse_rows(A, 50_000, 70_000, G2)["tiles"] >= 20_000 / 32
+
+
+SINGLE_ROWS = 16384  # SMFV_PLAN_SINGLE_ROWS
+
+
+def test_row_pair_tiles_on_host():
+    """(r5) Row pairs (the default; SMFV_PLAN_SINGLE_ROWS turns them off): a
+    k_rows_ws tile holds up to twice its teams in rows, the shortest riding
+    as second rows, and the native replay of the kernel's reads verifies
+    every plan (a failed check fails the call).  Short-row patterns stop at
+    the X-row and entry caps instead of the row count: about half the tiles
+    on a 0-7-entry band, 14 % fewer on the irregular cop20k_A stand-in;
+    geometries 1 / 2 / 3, a row block starting mid-matrix, tiny patterns."""
+    from conftest import short_rows_band
+    A = short_rows_band(20000, 3)
+    for g in (1024, 2048, 4096):
+        pr, one = _analyse_rows(A, 0, A.numRows, g), _analyse_rows(A, 0, A.numRows, g | SINGLE_ROWS)
+        assert pr["direct"] == one["direct"] == 0
+        assert pr["tiles"] <= 0.55 * one["tiles"] and pr["reuse"] > one["reuse"], (g, pr, one)
+    pr, one = _analyse_rows(A, 777, 15000), _analyse_rows(A, 777, 15000, SINGLE_ROWS)
+    assert pr["tiles"] <= 0.55 * one["tiles"]
+    B = smfv.inputs.cop20k_irregular_surrogate()
+    pr, one = _analyse_rows(B, 0, B.numRows), _analyse_rows(B, 0, B.numRows, SINGLE_ROWS)
+    assert one["tiles"] == 2441 and pr["tiles"] <= 0.9 * one["tiles"] and pr["direct"] == 0, (pr, one)
+    for name in ("empty7x5.mtx", "pat4x6.mtx", "sym5.mtx"):
+        C = smfv.readMatrixMarketFile(os.path.join(GOLDEN, name))
+        assert _analyse_rows(C, 0, C.numRows)["tiles"] >= 1, name
 
 
 def test_tile_analysis_unsorted_rows_with_repeats():
@@ -616,9 +645,13 @@ def test_ws_kernels_register_budget(tmp_path):
         name = re.search(r"\.name:\s+(\S+)", blk).group(1)
         if "k_rows_ws" not in name:
             continue
-        cw, lw = map(int, re.search(r"k_rows_ws(?:_live)?ILi(\d+)ELi(\d+)E", name).groups())
         vgpr = int(re.search(r"\.vgpr_count:\s+(\d+)", blk).group(1))
         spill = int(re.search(r"\.vgpr_spill_count:\s+(\d+)", blk).group(1))
+        geo = re.search(r"k_rows_ws(?:_live)?ILi(\d+)ELi(\d+)E", name)
+        if geo is None:  # (r5) k_rows_wsn: one 1024-lane block per CU
+            assert "k_rows_wsn" in name and vgpr <= 128 and spill == 0, (name, vgpr, spill)
+            continue
+        cw, lw = map(int, geo.groups())
         waves_per_simd = 4 if (cw, lw) in ((8, 8), (4, 4)) else 3
         assert vgpr <= 512 // waves_per_simd and spill == 0, (name, vgpr, spill)
         seen += 1
