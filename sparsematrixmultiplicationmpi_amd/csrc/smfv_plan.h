@@ -29,7 +29,7 @@ constexpr int TILE_KP = 32;
 // bank groups; a quad's value range ends after the last pair its rows sum.
 // ---------------------------------------------------------------------------
 constexpr int WS_UCAP = 239;     // union rows per tile
-constexpr int WS_NCAP = 1792;    // LDS entries per tile (u8 image row + f64 value)
+constexpr int WS_NCAP = 2048;    // LDS entries per tile (u8 image row + f64 value); (r5) 1792 -> 2048
 constexpr int WS_ROWS = 64;      // rows per tile
 constexpr int WS_LOADERS = 8;    // loader waves; each stages 8 x 1 KiB of X
 constexpr int WS_ZOFF = WS_UCAP * 256;  // byte offset of the zero row

@@ -251,10 +251,11 @@ def test_ws_geometry2_plans_verify():
     A = smfv.cop20k_surrogate()
     g1, g2 = _analyse_rows(A, 0, A.numRows, G1), _analyse_rows(A, 0, A.numRows, G2)
     assert g1 == _analyse_rows(A, 0, A.numRows)  # the default is geometry 1
-    # (r5) 2011 tiles of one row per team; 1960 with row pairs (the default)
-    assert _analyse_rows(A, 0, A.numRows, G1 | SINGLE_ROWS)["tiles"] == 2011
-    assert g1["tiles"] == 1960 and g2["direct"] == 0
-    assert 2.4 * g1["tiles"] < g2["tiles"] < 2.7 * g1["tiles"] and g2["reuse"] > 4.0
+    # (r5) 2010 tiles of one row per team (2011 with the r4 entry cap); 1860
+    # with row pairs (the default)
+    assert _analyse_rows(A, 0, A.numRows, G1 | SINGLE_ROWS)["tiles"] == 2010
+    assert g1["tiles"] == 1860 and g2["direct"] == 0
+    assert 2.4 * g1["tiles"] < g2["tiles"] < 2.9 * g1["tiles"] and g2["reuse"] > 4.0
     for name in ("empty7x5.mtx", "pat4x6.mtx"):
         B = smfv.readMatrixMarketFile(os.path.join(GOLDEN, name))
         assert _analyse_rows(B, 0, B.numRows, G2)["tiles"] >= 1, name
@@ -271,7 +272,7 @@ def test_row_pair_tiles_on_host():
     as second rows, and the native replay of the kernel's reads verifies
     every plan (a failed check fails the call).  Short-row patterns stop at
     the X-row and entry caps instead of the row count: about half the tiles
-    on a 0-7-entry band, 14 % fewer on the irregular cop20k_A stand-in;
+    on a 0-7-entry band, 18 % fewer on the irregular cop20k_A stand-in;
     geometries 1 / 2 / 3, a row block starting mid-matrix, tiny patterns."""
     from conftest import short_rows_band
     A = short_rows_band(20000, 3)
@@ -283,7 +284,7 @@ def test_row_pair_tiles_on_host():
     assert pr["tiles"] <= 0.55 * one["tiles"]
     B = smfv.inputs.cop20k_irregular_surrogate()
     pr, one = _analyse_rows(B, 0, B.numRows), _analyse_rows(B, 0, B.numRows, SINGLE_ROWS)
-    assert one["tiles"] == 2441 and pr["tiles"] <= 0.9 * one["tiles"] and pr["direct"] == 0, (pr, one)
+    assert one["tiles"] == 2333 and pr["tiles"] <= 0.85 * one["tiles"] and pr["direct"] == 0, (pr, one)
     for name in ("empty7x5.mtx", "pat4x6.mtx", "sym5.mtx"):
         C = smfv.readMatrixMarketFile(os.path.join(GOLDEN, name))
         assert _analyse_rows(C, 0, C.numRows)["tiles"] >= 1, name
