@@ -1109,8 +1109,8 @@ def main() -> None:
                          "per CU (SMFV_PLAN_WS_GEOM1 / 2 / 3)")
     ap.add_argument("--live-values", action="store_true",
                     help="tiled plans read the live CSR values (SMFV_PLAN_LIVE_VALUES: no snapshot, bind a no-op)")
-    ap.add_argument("--single-rows", action="store_true",
-                    help="one row per k_rows_ws team: no row pairs (SMFV_PLAN_SINGLE_ROWS, A/B)")
+    ap.add_argument("--row-pairs", default="auto", choices=["auto", "on", "off"],
+                    help="row pairs in k_rows_ws tiles: the plan with fewer rounds (auto), forced on / off (A/B)")
     ap.add_argument("--fma", action="store_true",
                     help="time the opt-in FMA plans (SMFV_PLAN_FMA) instead of the bit-exact ones")
     ap.add_argument("--rank-plans", type=int, default=0,
@@ -1214,7 +1214,7 @@ def main() -> None:
         plan = smfv.SpmmPlan(smfv.Variant[variant], dA, K, tiles=args.tiles, fma=args.fma, seeds=args.seeds,
                              mfma=args.mfma, split_ends=args.split_ends, xcd_parts=args.xcd_parts,
                              tiled_kernel=args.tiled_kernel, live_values=args.live_values,
-                             single_rows=args.single_rows)
+                             row_pairs=args.row_pairs)
         torch.cuda.synchronize()
         t_plan.append(time.time() - t0)
         copies.append((plan, dX, dY))

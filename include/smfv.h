@@ -212,14 +212,19 @@ typedef struct smfv_plan_s *smfv_plan_t;
  * plan).  Bit-identical to the snapshot path.  Tiled k_rows_ws plans only
  * (K = 1 chunk plans and SMFV_PLAN_MFMA keep their snapshot). */
 #define SMFV_PLAN_LIVE_VALUES 8192
-/* (r5) Without this flag a k_rows_ws tile may hold up to twice its teams in
- * rows: the shortest rows ride as second rows of the teams of the next
- * shortest (a team sums its first row, stores it, then sums its second), so
- * the tiles of short-row patterns stop at the X-row and entry caps instead of
- * the row count.  Same per-row order: bit-identical.  Snapshot plans only
- * (live-values plans keep one row per team).  This flag keeps one row per
- * team (A/B). */
+/* (r5) Row pairs: a k_rows_ws tile may hold up to twice its teams in rows,
+ * the shortest rows riding as second rows of the teams of the next shortest
+ * (a team sums its first row, stores it, then sums its second; no pair runs
+ * more than one batch of 8 past the tile's longest row), with a larger entry
+ * cap (2,048 against 1,792), so the tiles of short-row patterns stop at the
+ * X-row cap instead of the row count.  Same per-row order: bit-identical.
+ * Without either flag a plan builds both and keeps the one whose busiest
+ * block runs fewer tiles (ties: one row per team): the irregular cop20k
+ * stand-in pairs (10 -> 8 rounds, 27.6 -> 25.7 us), the stencil one does not
+ * (8 rounds either way, and bigger tiles make longer units).  SINGLE_ROWS
+ * forces one row per team, ROW_PAIRS forces pairs (A/B, tests). */
 #define SMFV_PLAN_SINGLE_ROWS 16384
+#define SMFV_PLAN_ROW_PAIRS 32768
 SMFV_API int smfv_plan_create(smfv_plan_t *plan, int variant, int m, int n, int64_t nnz,
                               const int *h_row_ptr, const int *h_col_idx, int K, int flags);
 /* Plan of the row block [row_begin, row_end) of a CSR matrix (h_row_ptr /
@@ -244,7 +249,8 @@ SMFV_API int smfv_plan_bind_values(smfv_plan_t plan, const double *d_values, voi
 SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_col_idx,
                                double out[6]);
 /* The same for the row block [row_begin, row_end) with the caps a plan of
- * these flags uses (smfv_plan_create_rows): out[0..5] as above, [6] XCD
+ * these flags uses (smfv_plan_create_rows; (r5) SMFV_PLAN_LIVE_VALUES builds
+ * and verifies the live-values layout): out[0..5] as above, [6] XCD
  * parts (8 or 1), [7] X footprint of the 8 parts (-1: not computed),
  * [8] X footprint of the plan's 8 XCD tile ranges (distinct X rows each
  * reads, summed, over the block's distinct X rows).  No device needed. */

@@ -1,7 +1,7 @@
 #!/bin/bash
 # (r5) Row pairs: the parity tests that run the tiled kernels, then an A/B on
-# one box -- new build (pairs), the same build with --single-rows (one row
-# per team: the plan effect alone), and the previous build (libsmfv_ab.so:
+# one box -- new build (automatic choice), the same build with pairs forced
+# on / off (the plan effect alone), and the previous build (libsmfv_ab.so:
 # the kernel change) -- alternating, per config.
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 out=gpurun_out/pairs
@@ -16,7 +16,8 @@ for cfg in ${CFGS:-cop20kirr_k32 cop20k_k32 cop20k_k128}; do
     for leg in ${LEGS:-new single old}; do
       case $leg in
         new) L=libsmfv.so; E="" ;;
-        single) L=libsmfv.so; E="--single-rows" ;;
+        pairs) L=libsmfv.so; E="--row-pairs on" ;;
+        single) L=libsmfv.so; E="--row-pairs off" ;;
         old) L=libsmfv_ab.so; E="" ;;
       esac
       SMFV_LIB=$L timeout -k 10 200 python bench.py --config $cfg --no-cpu-baseline --no-vendor --no-copy-floor \

@@ -799,8 +799,8 @@ __device__ __forceinline__ void ws_body(int xfirst, int xend, int npanel, int ch
         int row = R[slot];
         // (r5) a team may sum a second row after its first (row pairs: the
         // record's [3R, 4R), -1 none; its entries start at the batch after the
-        // first row's last); snapshot plans only
-        const int pw = LIVE ? -1 : R[3 * L::R + slot];
+        // first row's last)
+        const int pw = R[3 * L::R + slot];
         int info = R[L::R + slot], vw = R[2 * L::R + slot];
         for (; row >= 0;) {
             // the row runs nbat whole batches of 8, then rem (0, 2, 4 or 6)
@@ -831,6 +831,19 @@ __device__ __forceinline__ void ws_body(int xfirst, int xend, int npanel, int ch
             // halves (row * 256 = the byte offset), the address adds take
             // them as words (SDWA), as they did for u16 offsets
             const unsigned xo0 = (unsigned)(xb0 - lds), xo1 = (unsigned)(xb1 - lds);
+            // (stored before the barrier, while the loaders wait for their
+            // DMAs: stores deferred into the next unit, among the loaders'
+            // DMA issue, measured 25.6 -> 28.1 us)
+            auto store = [&](int r, d2 s0, d2 s1) {
+                double *y = Y + (int64_t)r * ldy + p * TILE_KP + 2 * tl;
+                if constexpr (NARROW) {
+                    if (2 * tl < kwin)  // columns 2 tl, 2 tl + 1 of the window (from either image half)
+                        __builtin_nontemporal_store(s0, reinterpret_cast<d2 *>(y));
+                } else {
+                    __builtin_nontemporal_store(s0, reinterpret_cast<d2 *>(y + 16 * par));
+                    __builtin_nontemporal_store(s1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
+                }
+            };
             auto rdx = [&](unsigned w, unsigned sel, d2 &a0, d2 &a1, d2 &b0, d2 &b1) {
                 const unsigned pw = __builtin_amdgcn_perm(0u, w, sel);
                 unsigned r0, r1, r2, r3;
@@ -918,24 +931,14 @@ __device__ __forceinline__ void ws_body(int xfirst, int xend, int npanel, int ch
                     }
                 }
             }
-            // (stored before the barrier, while the loaders wait for their
-            // DMAs: stores deferred into the next unit, among the loaders'
-            // DMA issue, measured 25.6 -> 28.1 us)
-            double *y = Y + (int64_t)row * ldy + p * TILE_KP + 2 * tl;
-            if constexpr (NARROW) {
-                if (2 * tl < kwin)  // columns 2 tl, 2 tl + 1 of the window (from either image half)
-                    __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y));
-            } else {
-                __builtin_nontemporal_store(acc0, reinterpret_cast<d2 *>(y + 16 * par));
-                __builtin_nontemporal_store(acc1, reinterpret_cast<d2 *>(y + 16 * (par ^ 1)));
-            }
-            if (LIVE || pw < 0 || row == (pw & 0xFFFFFF)) break;
+            store(row, acc0, acc1);
+            if (pw < 0 || row == (pw & 0xFFFFFF)) break;
             // the second row: from the batch after the first row's last (an
-            // empty first row owns one batch)
+            // empty first row owns one batch); LIVE: its odd-length flag
             const int nb = max(1, (len + 7) >> 3);
             row = pw & 0xFFFFFF;
-            info = (js + 4 * nb) | ((pw >> 24) << 16);
-            vw += 16 * nb;
+            info = (js + 4 * nb) | (((pw >> 24) & 63) << 16);
+            vw = LIVE ? (((vw & 0xFFFF) + 16 * nb) | (pw & (1 << 30))) : vw + 16 * nb;
         }
         if (++p == npanel) p = 0, ++it;
         barrier_lds();  // X slot (u & 1) is free for unit u + 2, meta slot for tile it + 1
@@ -2008,7 +2011,8 @@ static TileCaps plan_caps(int flags, int col_base)
     caps.frontier = !(flags & SMFV_PLAN_NATURAL_SEEDS);
     caps.split_ends = (flags & SMFV_PLAN_SPLIT_ENDS) ? SMFV_WS_BLOCKS_PER_XCD : 0;
     caps.col_base = col_base;  // a row block's neighbours are its columns shifted by its first global row
-    caps.pairs = !(flags & SMFV_PLAN_SINGLE_ROWS);
+    // (r5) row pairs: forced off / on, or the plan that runs fewer rounds
+    caps.pairs = (flags & SMFV_PLAN_SINGLE_ROWS) ? 0 : (flags & SMFV_PLAN_ROW_PAIRS) ? 1 : 2;
     return caps;
 }
 
@@ -2583,6 +2587,7 @@ SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int
     double footprint = -1.0;
     TileCaps caps = plan_caps(flags, row_begin);
     plan_parts(caps, flags, m, n, h_row_ptr, h_col_idx, &footprint);
+    caps.live = (flags & SMFV_PLAN_LIVE_VALUES) != 0;  // (r5) the live-values layout (WsPlan::vidx)
     TileAnalysis T;
     analyse_tiles(m, n, h_row_ptr, h_col_idx, T, caps);
     // invariants of the clustered analysis the plan is built from

@@ -64,6 +64,7 @@ struct ColumnRows {
 // Per-thread state of the greedy (column- and row-indexed stamps).
 struct TileScratch {
     std::vector<int> ustamp, upos, cstamp, rstamp, fresh, inner;
+    std::vector<int> hist, fit, small;  // (r5) row-pair check (analyse_part)
     std::vector<int64_t> probe;
     int64_t probe_id = 0;
     TileScratch(int m, int n)
@@ -159,6 +160,40 @@ bool analyse_part(int part, int lo, int hi, const int *P, int m, const int *rp, 
         };
         add_row(seed);
         const bool over = ucount > caps.ucap || tpad > caps.ncap;
+        // (r5) row pairs: a tile of n > team_rows rows sums its 2 np = 2 (n -
+        // team_rows) shortest rows two to a team, the i-th longest of them
+        // with the i-th shortest (build_ws_plan).  A row may join only if that
+        // pairing keeps every pair within the whole batches of the tile's
+        // longest row (which paces its unit) and every second row within
+        // pair_len non-zeros.  The check depends on the joining row's batch
+        // count only: computed once per count per step, on a histogram
+        auto nbat = [&](int r) { return std::max(1, (rp[r + 1] - rp[r] + 7) >> 3); };
+        constexpr int HB = 256;  // batch counts kept (longer rows never pair)
+        if (caps.team_rows > 0) {
+            S.hist.assign(HB + 1, 0);
+            S.hist[std::min(nbat(seed), HB)]++;
+        }
+        int bmax = nbat(seed);
+        const int bpair = std::max(1, caps.pair_len / 8);  // a second row: at most this many whole batches
+        int fit_step = -1;
+        auto pairs_fit = [&](int b) -> bool {  // rows + 1 (a row of b batches): do the pairs fit?
+            const int np = (int)rows.size() + 1 - caps.team_rows;
+            if (caps.team_rows <= 0 || np <= 0) return true;
+            if (fit_step != (int)rows.size()) fit_step = (int)rows.size(), S.fit.assign(HB + 1, -1);
+            const int bc = std::min(b, HB);
+            if (S.fit[bc] >= 0) return S.fit[bc] != 0;
+            // the 2 np shortest batch counts, ascending
+            S.small.clear();
+            for (int v = 1; v <= HB && (int)S.small.size() < 2 * np; ++v)
+                for (int c = S.hist[v] + (v == bc ? 1 : 0); c > 0 && (int)S.small.size() < 2 * np; --c)
+                    S.small.push_back(v);
+            bool ok = (int)S.small.size() == 2 * np;
+            const int lim = std::max(bmax, b) + caps.pair_slack;
+            for (int i = 0; ok && i < np; ++i)
+                ok = S.small[i] <= bpair && S.small[i] + S.small[2 * np - 1 - i] <= lim;
+            S.fit[bc] = ok ? 1 : 0;
+            return ok;
+        };
         while (!over && (int)rows.size() < caps.maxrows) {
             int best = -1, best_fresh = 1 << 30;
             long best_score = 1L << 40;
@@ -169,7 +204,7 @@ bool analyse_part(int part, int lo, int hi, const int *P, int m, const int *rp, 
                 // non-zeros (re-use 5.73 -> 5.80 on the cop20k_A surrogate)
                 const int len = rp[r + 1] - rp[r];
                 const long score = (long)S.fresh[r] * 64 - S.inner[r] * 16 - len;
-                if (score < best_score || (score == best_score && r < best)) {
+                if ((score < best_score || (score == best_score && r < best)) && pairs_fit(nbat(r))) {
                     best_score = score;
                     best_fresh = S.fresh[r];
                     best = r;
@@ -181,6 +216,7 @@ bool analyse_part(int part, int lo, int hi, const int *P, int m, const int *rp, 
                 while (next_free < hi && assigned[P[next_free]]) ++next_free;
                 if (next_free >= hi) break;
                 best = P[next_free];
+                if (!pairs_fit(nbat(best))) break;
                 score_terms(best);
                 best_fresh = S.fresh[best];
             }
@@ -188,6 +224,8 @@ bool analyse_part(int part, int lo, int hi, const int *P, int m, const int *rp, 
                 tpad + ((rp[best + 1] - rp[best] + caps.pad - 1) & ~(caps.pad - 1)) > caps.ncap)
                 break;
             add_row(best);
+            if (caps.team_rows > 0) S.hist[std::min(nbat(best), HB)]++;
+            bmax = std::max(bmax, nbat(best));
         }
         if (caps.frontier)
             for (int r : cand)
@@ -389,7 +427,7 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
             seen[r] = 1;
             if (pw == -1) continue;
             const int r2 = pw & 0xFFFFFF;
-            if (P.live || pw < 0 || r2 >= m || seen[r2]) return fail("second row out of range or repeated");
+            if (pw < 0 || r2 >= m || seen[r2]) return fail("second row out of range or repeated");
             seen[r2] = 1;
         }
     }
@@ -457,8 +495,9 @@ bool verify_ws_plan(int m, int n, const int *rp, const int *ci, const WsPlan &P,
             if (pw != -1) {
                 // the second row starts at the batch after the first row's
                 // last (an empty first row still owns one batch)
-                const int nb = std::max(1, (len + 7) / 8);
-                if (const char *e = check_row(pw & 0xFFFFFF, lb + 4 * nb, pw >> 24, vb + 16 * nb, k)) return e;
+                const int nb = std::max(1, (len + 7) / 8), r2 = pw & 0xFFFFFF;
+                if ((pw & (1 << 30)) != (P.live && (rp[r2 + 1] - rp[r2]) % 2 ? 1 << 30 : 0)) return "second row value flags";
+                if (const char *e = check_row(r2, lb + 4 * nb, (pw >> 24) & 63, vb + 16 * nb, k)) return e;
             }
         }
         return nullptr;
@@ -543,7 +582,11 @@ double parts_footprint(int m, int n, const int *rp, const int *ci, const std::ve
     return (double)sum / (double)total;
 }
 
-bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::string *err, const TileCaps &caps)
+namespace {
+// one k_rows_ws plan: one row per team or row pairs (caps.pairs 0 / 1),
+// tiles laid out within tcap entries
+bool build_ws_plan_one(int m, int n, const int *rp, const int *ci, WsPlan &P, std::string *err, const TileCaps &caps,
+                       int tcap)
 {
     // SMFV_PLAN_TIMING=1: the phases' host times on stderr (diagnostic)
     static const bool timing = std::getenv("SMFV_PLAN_TIMING") != nullptr;
@@ -566,12 +609,13 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     // (r5) row pairs: a tile may hold up to twice the kernel's teams in rows;
     // the rows past one per team go, shortest first, as second rows to the
     // teams of the next-shortest (the row index and its even length share
-    // one record word: < 2^24 rows, second rows of <= 126 entries)
-    const bool pairs = caps.pairs && !caps.live && m < (1 << 24);
+    // one record word: < 2^24 rows, second rows of <= 62 entries, bit 30 the
+    // live-values odd-length flag)
+    const bool pairs = caps.pairs == 1 && m < (1 << 24);
     TileAnalysis T;
     {
         TileCaps ac = caps;  // ucap / ncap / maxrows follow caps.geom (plan_caps)
-        if (pairs) ac.maxrows = 2 * G.rows();
+        if (pairs) ac.maxrows = 2 * G.rows(), ac.team_rows = G.rows(), ac.pair_len = caps.pair_len;
         analyse_tiles(m, n, rp, ci, T, ac);
     }
     tick("analyse_tiles");
@@ -608,8 +652,10 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
             // the 2 np shortest rows in np teams, the i-th longest with the
             // i-th shortest (even team lengths)
             const size_t n = R.size(), np = n - (size_t)NR, b = n - 2 * np;
-            for (size_t i = 0; i < np; ++i)
-                if (len2(R[n - 1 - i]) > 126) return false;
+            for (size_t i = 0; i < np; ++i)  // (no pair longer than the longest row; 6-bit second lengths)
+                if (len2(R[n - 1 - i]) > 62 || std::min(len8(R[b + i]), 8 * 256) + len8(R[n - 1 - i]) >
+                                                      len8(R[0]) + 8 * caps.pair_slack)
+                    return false;
             for (size_t i = 0; i < np; ++i) partner[(size_t)R[b + i]] = R[n - 1 - i];
             R.resize(n - np);
             std::sort(R.begin(), R.end(), [&](int a, int b) {
@@ -627,7 +673,7 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     };
     auto fits = [&](const std::vector<int> &R) {
         std::vector<int> h = R;
-        return make_teams(h) && layout(h) <= G.ncap;
+        return make_teams(h) && layout(h) <= tcap;
     };
     // value entries of a quad: its offsets' 32 per batch, less the value
     // pairs of its last batch that no row sums (pair groups q >= qmax of a
@@ -701,14 +747,18 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
                         if (!P.live) P.tsrc[(size_t)(vnoff + (int64_t)(vbase + 4 * (el / 2) + k) * 2 + el % 2)] = j;
                     }
                 const int rl = rp[r + 1] - rp[r];
-                if (P.live)  // (r5) value slot of pair c: its first entry's CSR index
+                if (P.live) {  // (r5) value slot of pair c: its first entry's CSR index
                     for (int c = 0; c < len2(r) / 2; ++c) P.vidx[(size_t)t * P.vstride + vbase + 4 * c + k] = rp[r] + 2 * c;
+                    if (r2 >= 0)  // the second row's pairs from the batch after the first row's last
+                        for (int c = 0; c < len2(r2) / 2; ++c)
+                            P.vidx[(size_t)t * P.vstride + vbase + 2 * len8(r) + 4 * c + k] = rp[r2] + 2 * c;
+                }
                 lrec[slot] = r;
                 lrec[NR + slot] = lbase | (len2(r) << 16);
                 lrec[2 * NR + slot] = vbase | (P.live && rl % 2 ? 1 << 30 : 0);
                 tiled += rl;
                 if (r2 >= 0) {
-                    lrec[3 * NR + slot] = r2 | (len2(r2) << 24);
+                    lrec[3 * NR + slot] = r2 | (len2(r2) << 24) | (P.live && (rp[r2 + 1] - rp[r2]) % 2 ? 1 << 30 : 0);
                     tiled += rp[r2 + 1] - rp[r2];
                 }
             }
@@ -878,6 +928,38 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
     const bool ok = verify_ws_plan(m, n, rp, ci, P, err);
     tick("verify");
     return ok;
+}
+}  // namespace
+
+bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::string *err, const TileCaps &caps)
+{
+    // caps.ncap leaves the quads' interleave room below geom.ncap; a plan of
+    // one row per team keeps the same room below geom.ncap1
+    const WsGeom G = caps.geom;
+    auto one = [&](WsPlan &Q, int pairs, std::string *e) {
+        TileCaps c = caps;
+        c.pairs = pairs;
+        const int tcap = pairs ? G.ncap : G.ncap1;
+        c.ncap = caps.ncap - (G.ncap - tcap);
+        return build_ws_plan_one(m, n, rp, ci, Q, e, c, tcap);
+    };
+    if (caps.pairs != 2) return one(P, caps.pairs, err);
+    // (r5) both, and the one whose busiest block runs fewer tiles: a round
+    // of units costs about the same whatever the tiles hold, and bigger
+    // tiles make longer units (measured: row pairs 27.6 -> 25.7 us on the
+    // irregular stand-in, 10 -> 8 rounds; 23.5 -> 24.0 us on the stencil
+    // one, 8 rounds either way)
+    auto rounds = [&](const WsPlan &Q) {
+        int r = 0;
+        for (int x = 0; x < 8; ++x)
+            r = std::max(r, (Q.xcd[x + 1] - Q.xcd[x] + std::max(1, caps.xcd_blocks) - 1) / std::max(1, caps.xcd_blocks));
+        return r;
+    };
+    if (!one(P, 0, err)) return false;
+    WsPlan Q;
+    std::string e2;  // (a pair plan that fails its checks is not taken)
+    if (one(Q, 1, &e2) && rounds(Q) < rounds(P)) P = std::move(Q);
+    return true;
 }
 
 // ---------------------------------------------------------------------------

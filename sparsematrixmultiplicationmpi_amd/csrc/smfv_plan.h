@@ -43,8 +43,9 @@ constexpr int WS_GWORDS = 352, WS_G_NOFF = 256, WS_G_TN = 272, WS_G_NU = 288, WS
 // tile, [0, R) row per team slot (-1 none), [R, 2R) L chunk base | (padded
 // length << 16), [2R, 3R) V chunk base; team slot = team-in-wave * (compute
 // waves) + wave; (r5) [3R, 4R) the team's second row | its length (rounded
-// up to even) << 24, or -1: the team sums it after the first, from the batch
-// after the first row's last (TileCaps::pairs)
+// up to even, <= 62) << 24 | (live values) its odd-length flag << 30, or -1:
+// the team sums it after the first, from the batch after the first row's
+// last (TileCaps::pairs)
 constexpr int WS_LWORDS = 256;
 constexpr int WS_SLACK = 2048;   // entries past the end (DMA over-read of the last tile)
 
@@ -63,14 +64,15 @@ constexpr int WS_SLACK = 2048;   // entries past the end (DMA over-read of the l
 //             to 168 VGPRs and the compute waves run a deeper read-ahead.
 struct WsGeom {
     int id, cw, lw, ppw, ucap, ncap, xcd_blocks;
+    int ncap1;  // (r5) entry cap of a plan of one row per team (row-pair plans take ncap)
     constexpr int rows() const { return 8 * cw; }
     constexpr int threads() const { return 64 * (cw + lw); }
     // global record word of loader wave w, lane quarter q, piece i (union id 4 (w + lw i) + q)
     constexpr int gword(int w, int q, int i) const { return 4 * ppw * w + ppw * q + i; }
 };
-constexpr WsGeom WS_GEOM1{1, 8, 8, 8, WS_UCAP, WS_NCAP, 32};
-constexpr WsGeom WS_GEOM2{2, 4, 4, 8, 125, 896, 64};
-constexpr WsGeom WS_GEOM3{3, 8, 4, 16, WS_UCAP, WS_NCAP, 32};
+constexpr WsGeom WS_GEOM1{1, 8, 8, 8, WS_UCAP, WS_NCAP, 32, 1792};
+constexpr WsGeom WS_GEOM2{2, 4, 4, 8, 125, 896, 64, 896};
+constexpr WsGeom WS_GEOM3{3, 8, 4, 16, WS_UCAP, WS_NCAP, 32, 1792};
 constexpr WsGeom ws_geom(int id) { return id == 2 ? WS_GEOM2 : id == 3 ? WS_GEOM3 : WS_GEOM1; }
 
 // Per-tile summary of the clustered analysis.
@@ -127,9 +129,20 @@ struct TileCaps {
     int xcd_blocks = 32;           // k_rows_ws blocks per XCD (MI355X: 256 CUs / 8 XCDs)
     WsGeom geom = WS_GEOM1;        // build_ws_plan: the kernel geometry (ucap / ncap / maxrows follow it)
     bool live = false;             // build_ws_plan: live values (WsPlan::vidx) instead of a snapshot (tsrc)
-    // (r5) build_ws_plan: tiles of up to 2 x geom.rows() rows, a team summing
-    // two short rows one after the other (snapshot plans of < 2^24 rows)
-    bool pairs = false;
+    // (r5) build_ws_plan: row pairs -- tiles of up to 2 x geom.rows() rows,
+    // a team summing two short rows one after the other (plans of < 2^24
+    // rows), entry cap geom.ncap -- 0 never (one row per team, entry cap
+    // geom.ncap1), 1 always, 2 whichever plan runs fewer rounds of tiles per
+    // block (ties: one row per team)
+    int pairs = 0;
+    // (r5) analyse_tiles: a tile of n > team_rows rows (team_rows 0: no
+    // limit) pairs its 2 (n - team_rows) shortest rows, the i-th longest with
+    // the i-th shortest; a row joins only if no pair then outlasts the tile's
+    // longest row by more than pair_slack batches and no second row has more than pair_len
+    // non-zeros (rounded down to whole batches)
+    int team_rows = 0;
+    int pair_len = 56;
+    int pair_slack = 1;            // batches a pair may run past the longest row
 };
 // Independent parts are analysed on up to 8 threads; analysis_threads > 0
 // caps that for analyses run on the calling thread (smfv_set_analysis_threads).

@@ -120,6 +120,7 @@ PLAN_ONE_WAVEFRONT, PLAN_SIMPLE_ROWS, PLAN_CS, PLAN_WS = 64, 128, 256, 512
 PLAN_WS_GEOM1, PLAN_WS_GEOM2, PLAN_WS_GEOM3 = 1024, 2048, 4096
 PLAN_LIVE_VALUES = 8192  # (r5) the tiled kernel reads the live CSR values (no snapshot, no bind)
 PLAN_SINGLE_ROWS = 16384  # (r5) one row per k_rows_ws team (no row pairs; A/B)
+PLAN_ROW_PAIRS = 32768  # (r5) row pairs forced (without either: the plan with fewer rounds)
 PLAN_STATS = 18  # SMFV_PLAN_STATS
 PLAN_KERNELS = {0: None, 1: "k_rows_ws", 2: "k_rows_mfma", 3: "k_spmv_chunks", 5: "k_rows_wsn"}
 
@@ -143,14 +144,15 @@ class SpmmPlan:
                  stream: torch.cuda.Stream | None = None, rows: tuple[int, int] | None = None,
                  seeds: str = "frontier", mfma: bool = False, split_ends: bool = False,
                  xcd_parts: str = "auto", tiled_kernel: str = "auto", live_values: bool = False,
-                 single_rows: bool = False):
+                 row_pairs: str = "auto"):
         self.variant, self.A, self.K = Variant(variant), A, K
         self.rows = rows
         flags = {"auto": 0, "off": PLAN_NO_TILES, "force": PLAN_FORCE_TILES}[tiles]
         if live_values:  # (r5) SMFV_PLAN_LIVE_VALUES: value pairs DMA'd from the CSR values, bind a no-op
             flags |= PLAN_LIVE_VALUES
-        if single_rows:  # (r5) one row per k_rows_ws team, no row pairs (SMFV_PLAN_SINGLE_ROWS, A/B)
-            flags |= PLAN_SINGLE_ROWS
+        # (r5) row pairs in k_rows_ws tiles: "auto" (the plan whose busiest
+        # block runs fewer tiles), "off" (SMFV_PLAN_SINGLE_ROWS), "on" (SMFV_PLAN_ROW_PAIRS)
+        flags |= {"auto": 0, "off": PLAN_SINGLE_ROWS, "on": PLAN_ROW_PAIRS}[row_pairs]
         if fma:  # opt-in fused multiply-add in the tiled kernel: within tolerance, not bit-identical
             flags |= PLAN_FMA
         if seeds == "natural":  # tiles seeded in row order (A/B of the wavefront seeding)

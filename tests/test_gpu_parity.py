@@ -1031,12 +1031,14 @@ def test_narrow_team_tiles(gpu, K):
 @pytest.mark.parametrize("tk", ["auto", "ws2", "ws3"])
 def test_row_pair_tiles(gpu, tk):
     """(r5) Row pairs: teams summing a second (short) row after their first
-    (the default; SMFV_PLAN_SINGLE_ROWS keeps one row per team) -- on a
+    (SMFV_PLAN_ROW_PAIRS; SMFV_PLAN_SINGLE_ROWS keeps one row per team;
+    neither: the plan with fewer rounds of tiles per block) -- on a
     0-7-entry band with long rows (every residue, empty rows), a row block
     starting mid-matrix and the irregular cop20k_A stand-in; K = 32 / 64 /
     128 and a 16-column window of a wider X (NARROW): bit-identical to the
     reference's order and to the single-row plan, and after a value change
-    (the bind items re-gather the paired rows' values)."""
+    (the bind items re-gather the paired rows' values); live-values plans
+    pair rows too (odd-length second rows: their -0.0 write)."""
     from conftest import short_rows_band
     rng = np.random.default_rng(300)
     mats = [short_rows_band(20000, 3)] + ([smfv.inputs.cop20k_irregular_surrogate()] if tk == "auto" else [])
@@ -1049,12 +1051,13 @@ def test_row_pair_tiles(gpu, tk):
             r0, r1 = rows or (0, A.numRows)
             Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, Xw)[r0:r1]
             outs = []
-            for single in (False, True):
-                plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles="force", rows=rows, single_rows=single,
-                                     tiled_kernel="auto" if tk == "auto" else tk)
+            for pairs, live in (("on", False), ("off", False), ("on", True), ("auto", False)):
+                plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles="force", rows=rows, row_pairs=pairs,
+                                     tiled_kernel="auto" if tk == "auto" else tk, live_values=live)
                 st = plan.stats()
-                assert st["tiled"] and st["kernel"] == "k_rows_ws", st
-                assert (st["paired_rows"] > 0) != single, st
+                assert st["tiled"] and st["kernel"] == "k_rows_ws" and st["live_values"] == live, st
+                if pairs != "auto":
+                    assert (st["paired_rows"] > 0) == (pairs == "on"), st
                 Yb = torch.full((r1 - r0, K + 1), np.nan, dtype=torch.float64, device=gpu)
                 plan.run(dXf[:, f:f + K], Yb[:, :K])
                 torch.cuda.synchronize()
@@ -1063,7 +1066,7 @@ def test_row_pair_tiles(gpu, tk):
                 assert torch.isnan(Yb[:, K:]).all()
         # values changed: a re-bind gathers the paired rows' values too
         dA.values.mul_(-0.5)
-        plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, 32, tiles="force")
+        plan = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, 32, tiles="force", row_pairs="on")
         dA.values.mul_(-2.0)
         plan.bind_values()
         Y = torch.full((A.numRows, 32), np.nan, dtype=torch.float64, device=gpu)
@@ -1071,3 +1074,7 @@ def test_row_pair_tiles(gpu, tk):
         torch.cuda.synchronize()
         Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, np.ascontiguousarray(X[:, :32]))
         assert np.array_equal(bits(Y.cpu().numpy()), bits(Yref)), plan.stats()
+    if tk == "auto":  # the automatic choice: the irregular stand-in pairs (10 -> 8 rounds), the stencil does not
+        irr = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(mats[1], gpu), 32).stats()
+        sten = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(smfv.cop20k_surrogate(), gpu), 32).stats()
+        assert irr["paired_rows"] > 0 and sten["paired_rows"] == 0, (irr, sten)

@@ -251,11 +251,11 @@ def test_ws_geometry2_plans_verify():
     A = smfv.cop20k_surrogate()
     g1, g2 = _analyse_rows(A, 0, A.numRows, G1), _analyse_rows(A, 0, A.numRows, G2)
     assert g1 == _analyse_rows(A, 0, A.numRows)  # the default is geometry 1
-    # (r5) 2010 tiles of one row per team (2011 with the r4 entry cap); 1860
-    # with row pairs (the default)
-    assert _analyse_rows(A, 0, A.numRows, G1 | SINGLE_ROWS)["tiles"] == 2010
-    assert g1["tiles"] == 1860 and g2["direct"] == 0
-    assert 2.4 * g1["tiles"] < g2["tiles"] < 2.9 * g1["tiles"] and g2["reuse"] > 4.0
+    # (r5) row pairs: 1906 tiles, 8 rounds per block as 2011 tiles of one row
+    # per team, so the automatic choice keeps one row per team
+    assert _analyse_rows(A, 0, A.numRows, G1 | ROW_PAIRS)["tiles"] == 1906
+    assert g1["tiles"] == 2011 == _analyse_rows(A, 0, A.numRows, G1 | SINGLE_ROWS)["tiles"] and g2["direct"] == 0
+    assert 2.4 * g1["tiles"] < g2["tiles"] < 2.7 * g1["tiles"] and g2["reuse"] > 4.0
     for name in ("empty7x5.mtx", "pat4x6.mtx"):
         B = smfv.readMatrixMarketFile(os.path.join(GOLDEN, name))
         assert _analyse_rows(B, 0, B.numRows, G2)["tiles"] >= 1, name
@@ -263,31 +263,41 @@ def test_ws_geometry2_plans_verify():
     assert _analyse_rows(A, 50_000, 70_000, G2)["tiles"] >= 20_000 / 32
 
 
-SINGLE_ROWS = 16384  # SMFV_PLAN_SINGLE_ROWS
+SINGLE_ROWS, ROW_PAIRS = 16384, 32768  # SMFV_PLAN_SINGLE_ROWS / SMFV_PLAN_ROW_PAIRS
 
 
 def test_row_pair_tiles_on_host():
-    """(r5) Row pairs (the default; SMFV_PLAN_SINGLE_ROWS turns them off): a
+    """(r5) Row pairs (SMFV_PLAN_ROW_PAIRS; SMFV_PLAN_SINGLE_ROWS one row
+    per team; neither: the plan whose busiest block runs fewer tiles): a
     k_rows_ws tile holds up to twice its teams in rows, the shortest riding
     as second rows, and the native replay of the kernel's reads verifies
     every plan (a failed check fails the call).  Short-row patterns stop at
-    the X-row and entry caps instead of the row count: about half the tiles
-    on a 0-7-entry band, 18 % fewer on the irregular cop20k_A stand-in;
-    geometries 1 / 2 / 3, a row block starting mid-matrix, tiny patterns."""
+    the X-row cap instead of the row count: about half the tiles on a
+    0-7-entry band, 19 % fewer on the irregular cop20k_A stand-in (10 -> 8
+    rounds: the automatic choice pairs); geometries 1 / 2 / 3, a row block
+    starting mid-matrix, tiny patterns."""
     from conftest import short_rows_band
     A = short_rows_band(20000, 3)
     for g in (1024, 2048, 4096):
-        pr, one = _analyse_rows(A, 0, A.numRows, g), _analyse_rows(A, 0, A.numRows, g | SINGLE_ROWS)
+        pr, one = _analyse_rows(A, 0, A.numRows, g | ROW_PAIRS), _analyse_rows(A, 0, A.numRows, g | SINGLE_ROWS)
         assert pr["direct"] == one["direct"] == 0
         assert pr["tiles"] <= 0.55 * one["tiles"] and pr["reuse"] > one["reuse"], (g, pr, one)
-    pr, one = _analyse_rows(A, 777, 15000), _analyse_rows(A, 777, 15000, SINGLE_ROWS)
+        assert _analyse_rows(A, 0, A.numRows, g) == pr  # fewer rounds: the automatic choice pairs
+    pr, one = _analyse_rows(A, 777, 15000, ROW_PAIRS), _analyse_rows(A, 777, 15000, SINGLE_ROWS)
     assert pr["tiles"] <= 0.55 * one["tiles"]
     B = smfv.inputs.cop20k_irregular_surrogate()
-    pr, one = _analyse_rows(B, 0, B.numRows), _analyse_rows(B, 0, B.numRows, SINGLE_ROWS)
-    assert one["tiles"] == 2333 and pr["tiles"] <= 0.85 * one["tiles"] and pr["direct"] == 0, (pr, one)
+    pr, one = _analyse_rows(B, 0, B.numRows, ROW_PAIRS), _analyse_rows(B, 0, B.numRows, SINGLE_ROWS)
+    assert one["tiles"] == 2441 and pr["tiles"] <= 0.85 * one["tiles"] and pr["direct"] == 0, (pr, one)
+    assert _analyse_rows(B, 0, B.numRows) == pr
+    # live-values plans pair rows too (the second row's odd-length flag and
+    # value slots replayed): the same tiles as the snapshot plan
+    LIVE = 8192  # SMFV_PLAN_LIVE_VALUES
+    for M, r0, r1 in ((A, 0, A.numRows), (A, 777, 15000), (B, 0, B.numRows)):
+        assert _analyse_rows(M, r0, r1, LIVE | ROW_PAIRS)["tiles"] == _analyse_rows(M, r0, r1, ROW_PAIRS)["tiles"]
     for name in ("empty7x5.mtx", "pat4x6.mtx", "sym5.mtx"):
         C = smfv.readMatrixMarketFile(os.path.join(GOLDEN, name))
         assert _analyse_rows(C, 0, C.numRows)["tiles"] >= 1, name
+        assert _analyse_rows(C, 0, C.numRows, LIVE | ROW_PAIRS)["tiles"] >= 1, name
 
 
 def test_tile_analysis_unsorted_rows_with_repeats():
