@@ -51,6 +51,16 @@ double smfvInitDevice();
 double smfvDistributeInputs(SparseMatrix &A, FatVector &fatVector, int k);
 void smfvReleaseInputs();
 
+// (r5) Plans and their one-time cost.  The four functions cache one plan
+// per (pattern, variant, k).  With one rank the first call of a pattern runs
+// an untiled plan at once and the tiled plan is analysed on a background
+// thread for the later calls.  With several ranks no thread runs beside
+// RCCL: every rank builds its tiled distributed plan inside the pattern's
+// SECOND call (the host analysis, ~0.1-0.2 s on cop20k_A, lands in that
+// call's `prep`) and runs it from that call on.  That
+// multi-rank switch is covered by single-rank tests only here (mpiexec -n 1;
+// RCCL refuses two ranks on one GPU); a multi-GPU node runs it first.
+
 // Stage times (seconds) of the last call of the four functions on this rank,
 // recorded when the environment has SMFV_TIMING=1 (then rank 0 also prints
 // them, averaged over the ranks for the MPI variants, as the reference's
