@@ -19,6 +19,8 @@ for cfg in ${CFGS:-cop20kirr_k32 cop20k_k32 cop20k_k128}; do
         pairs) L=libsmfv.so; E="--row-pairs on" ;;
         single) L=libsmfv.so; E="--row-pairs off" ;;
         old) L=libsmfv_ab.so; E="" ;;
+        ws3) L=libsmfv.so; E="--tiled-kernel ws3" ;;
+        ws3old) L=libsmfv_ab.so; E="--tiled-kernel ws3" ;;
       esac
       SMFV_LIB=$L timeout -k 10 200 python bench.py --config $cfg --no-cpu-baseline --no-vendor --no-copy-floor \
           --no-rebind $E ${EXTRA:-} > $out/${cfg}_${leg}_$r.json 2> $out/${cfg}_${leg}_$r.log || exit $?
