@@ -1078,4 +1078,3 @@ def test_row_pair_tiles(gpu, tk):
         irr = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(mats[1], gpu), 32).stats()
         sten = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(smfv.cop20k_surrogate(), gpu), 32).stats()
         assert irr["paired_rows"] > 0 and sten["paired_rows"] == 0, (irr, sten)
-
