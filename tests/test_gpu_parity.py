@@ -1078,3 +1078,26 @@ def test_row_pair_tiles(gpu, tk):
         irr = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(mats[1], gpu), 32).stats()
         sten = smfv.SpmmPlan(smfv.Variant.ROWWISE, smfv.DeviceCSR(smfv.cop20k_surrogate(), gpu), 32).stats()
         assert irr["paired_rows"] > 0 and sten["paired_rows"] == 0, (irr, sten)
+
+
+def test_row_pairs_every_variant(gpu):
+    """(r5) Row pairs under every variant's single-device plan (SEQUENTIAL,
+    ROWWISE, COLUMNWISE, NONZERO over whole rows: the same tiled kernel,
+    bit-identical to the reference's order) and at K = 64 with a padded Y
+    (an even row stride: an odd one sends every plan to the untiled kernels,
+    and NONZERO's to the merge path, pick_vec)."""
+    from conftest import short_rows_band
+    A = short_rows_band(12000, 9)
+    K = 64
+    X = np.random.default_rng(9).uniform(-1, 1, (A.numCols, K))
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+    dA, dX = smfv.DeviceCSR(A, gpu), torch.from_numpy(X).to(gpu)
+    for v in smfv.Variant:
+        plan = smfv.SpmmPlan(v, dA, K, tiles="force", row_pairs="on")
+        st = plan.stats()
+        assert st["tiled"] and st["paired_rows"] > 0, (v, st)
+        Yb = torch.full((A.numRows, K + 6), np.nan, dtype=torch.float64, device=gpu)
+        plan.run(dX, Yb[:, :K])
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(Yb[:, :K].cpu().numpy()), bits(Yref)), (v, st)
+        assert torch.isnan(Yb[:, K:]).all()
