@@ -955,10 +955,24 @@ bool build_ws_plan(int m, int n, const int *rp, const int *ci, WsPlan &P, std::s
             r = std::max(r, (Q.xcd[x + 1] - Q.xcd[x] + std::max(1, caps.xcd_blocks) - 1) / std::max(1, caps.xcd_blocks));
         return r;
     };
-    if (!one(P, 0, err)) return false;
+    // the two plans are built side by side (the pair plan on a second
+    // thread, with the caller's analysis-thread budget split between them)
     WsPlan Q;
     std::string e2;  // (a pair plan that fails its checks is not taken)
-    if (one(Q, 1, &e2) && rounds(Q) < rounds(P)) P = std::move(Q);
+    bool q_ok = false;
+    const int budget = analysis_threads > 0 ? analysis_threads : 8;
+    const int half = std::max(1, budget / 2);
+    std::thread other([&, half] {
+        analysis_threads = half;
+        q_ok = one(Q, 1, &e2);
+    });
+    const int saved = analysis_threads;
+    analysis_threads = std::max(1, budget - half);
+    const bool p_ok = one(P, 0, err);
+    analysis_threads = saved;
+    other.join();
+    if (!p_ok) return false;
+    if (q_ok && rounds(Q) < rounds(P)) P = std::move(Q);
     return true;
 }
 
