@@ -1148,23 +1148,41 @@ __global__ __launch_bounds__(1024, 1) void k_rows_wsn(WsXcd xr, const int *__res
         const int word = RR[wv * TW + k];
         if (word != -1) {
             const int row = word & 0xFFFFFF, nbat = (int)((unsigned)word >> 24);
-            const u4 *Lq = reinterpret_cast<const u4 *>(mbase + L::M_L) + RR[R + 2 * wv] + k;
+            // (r5) batches of WSN_B = 4 entries: 4 u16 image rows in one 8-byte
+            // read, two value pairs; X of batch b + 1 is read before batch b
+            // is summed
+            const u2 *Lq = reinterpret_cast<const u2 *>(mbase + L::M_L) + RR[R + 2 * wv] + k;
             const d2 *Vq = reinterpret_cast<const d2 *>(mbase + L::M_V) + RR[R + 2 * wv + 1] + k;
             d2 acc = {0.0, 0.0};
-            u4 ow = Lq[0];
-            for (int b = 0; b < nbat; ++b) {
-                d2 v[4], xx[8];
+            auto rdx = [&](u2 w, d2 (&x)[4]) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = Vq[(4 * b + q) * TW];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const unsigned w32 = e < 2 ? ow.x : e < 4 ? ow.y : e < 6 ? ow.z : ow.w;
+                for (int e = 0; e < 4; ++e) {
+                    const unsigned w32 = e < 2 ? w.x : w.y;
                     const unsigned off = (e & 1) ? (w32 >> 16) : (w32 & 0xFFFFu);
-                    xx[e] = *reinterpret_cast<const d2 *>(xbase + off * XROW);
+                    x[e] = *reinterpret_cast<const d2 *>(xbase + off * XROW);
                 }
-                if (b + 1 < nbat) ow = Lq[(b + 1) * TW];  // the next batch's offsets behind this batch's reads
-#pragma unroll
-                for (int e = 0; e < 8; ++e) acc = madd(acc, (e & 1) ? v[e >> 1].y : v[e >> 1].x, xx[e]);
+            };
+            d2 xa[4], xb[4];
+            rdx(Lq[0], xa);
+            u2 on = Lq[min(1, nbat - 1) * TW];
+            for (int b = 0; b < nbat; b += 2) {
+                // batch b in xa; batch b + 1's reads go out first
+                d2 v0 = Vq[(2 * b) * TW], v1 = Vq[(2 * b + 1) * TW];
+                rdx(on, xb);
+                on = Lq[min(b + 2, nbat - 1) * TW];
+                acc = madd(acc, v0.x, xa[0]);
+                acc = madd(acc, v0.y, xa[1]);
+                acc = madd(acc, v1.x, xa[2]);
+                acc = madd(acc, v1.y, xa[3]);
+                if (b + 1 < nbat) {
+                    v0 = Vq[(2 * b + 2) * TW], v1 = Vq[(2 * b + 3) * TW];
+                    rdx(on, xa);
+                    on = Lq[min(b + 3, nbat - 1) * TW];
+                    acc = madd(acc, v0.x, xb[0]);
+                    acc = madd(acc, v0.y, xb[1]);
+                    acc = madd(acc, v1.x, xb[2]);
+                    acc = madd(acc, v1.y, xb[3]);
+                }
             }
             __builtin_nontemporal_store(acc, reinterpret_cast<d2 *>(Y + (int64_t)row * ldy + 2 * tli));
         }

@@ -1205,12 +1205,13 @@ bool verify_wsn_plan(int m, int n, const int *rp, const int *ci, const WsnPlan &
                 if (r < 0 || r >= m || seen[r]) return fail("tile row out of range or repeated");
                 seen[r] = 1;
                 const int rl = rp[r + 1] - rp[r];
-                if (nbat != std::max(1, (rl + 7) / 8)) return fail("row batches");
+                if (nbat != std::max(1, (rl + WSN_B - 1) / WSN_B)) return fail("row batches");
                 for (int b = 0; b < nbat; ++b)
-                    for (int e = 0; e < 8; ++e) {
-                        const int el = 8 * b + e;
-                        const int64_t le = (int64_t)noff + 8 * (int64_t)(lb + b * TW + k) + e;
-                        const int64_t ve = (int64_t)voff + 2 * (int64_t)(vb + (4 * b + e / 2) * TW + k) + e % 2;
+                    for (int e = 0; e < WSN_B; ++e) {
+                        const int el = WSN_B * b + e;
+                        const int64_t le = (int64_t)noff + WSN_B * (int64_t)(lb + b * TW + k) + e;
+                        const int64_t ve =
+                            (int64_t)voff + 2 * (int64_t)(vb + (WSN_B / 2 * b + e / 2) * TW + k) + e % 2;
                         if (le >= noff + tn || ve >= voff + tnv) return fail("segment leaves its tile");
                         if (el < rl) {
                             const int j = rp[r] + el, u = P.loff[(size_t)le];
@@ -1252,7 +1253,7 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
     TileAnalysis T;
     analyse_tiles(m, n, rp, ci, T, caps);
 
-    auto nbat = [&](int r) { return std::max(1, (rp[r + 1] - rp[r] + 7) / 8); };
+    auto nbat = [&](int r) { return std::max(1, (rp[r + 1] - rp[r] + WSN_B - 1) / WSN_B); };
     auto by_length = [&](std::vector<int> &rows) {
         std::sort(rows.begin(), rows.end(), [&](int a, int b) {
             const int la = rp[a + 1] - rp[a], lb = rp[b + 1] - rp[b];
@@ -1261,7 +1262,7 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
     };
     auto layout = [&](const std::vector<int> &rows) {  // padded entries (rows sorted by decreasing length)
         int64_t e = 0;
-        for (size_t g = 0; g < rows.size(); g += (size_t)TW) e += (int64_t)nbat(rows[g]) * TW * 8;
+        for (size_t g = 0; g < rows.size(); g += (size_t)TW) e += (int64_t)nbat(rows[g]) * TW * WSN_B;
         return e;
     };
     std::vector<std::vector<int>> tiles, stack;
@@ -1333,7 +1334,7 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
         for (int s = 0; s < R; ++s) l[s] = -1;
         // wave group q (TW consecutive rows of the sorted list) -> wave w;
         // groups q and 7 - q share a SIMD (waves w and w + 4)
-        int64_t chunk = 0;  // 16-byte offset chunks so far (= 8 entries each)
+        int64_t chunk = 0;  // offset chunks so far (WSN_B entries each)
         int lbase[8] = {}, vbase[8] = {}, wnb[8] = {};
         for (int q = 0; q < 8 && (size_t)q * TW < Rw.size(); ++q) {
             const int w = q < 4 ? q : 11 - q;
@@ -1344,7 +1345,7 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
             lbase[w] = (int)chunk;
             vbase[w] = (int)vchunk;
             chunk += (int64_t)wnb[w] * TW;
-            vchunk += (int64_t)wnb[w] * 4 * TW;
+            vchunk += (int64_t)wnb[w] * (WSN_B / 2) * TW;
         }
         for (int q = 0; q < 8 && (size_t)q * TW < Rw.size(); ++q) {
             const int w = q < 4 ? q : 11 - q;
@@ -1352,9 +1353,9 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
                 const int r = Rw[(size_t)(q * TW + k)];
                 l[w * TW + k] = r | (nbat(r) << 24);
                 for (int j = rp[r]; j < rp[r + 1]; ++j) {
-                    const int el = j - rp[r], b = el / 8, e = el % 8;
-                    P.loff[(size_t)(noff + 8 * (int64_t)(lbase[w] + b * TW + k) + e)] = (uint16_t)pos[ci[j]];
-                    P.tsrc[(size_t)(noff + 2 * (int64_t)(vbase[w] + (4 * b + e / 2) * TW + k) + e % 2)] = j;
+                    const int el = j - rp[r], b = el / WSN_B, e = el % WSN_B;
+                    P.loff[(size_t)(noff + WSN_B * (int64_t)(lbase[w] + b * TW + k) + e)] = (uint16_t)pos[ci[j]];
+                    P.tsrc[(size_t)(noff + 2 * (int64_t)(vbase[w] + (WSN_B / 2 * b + e / 2) * TW + k) + e % 2)] = j;
                 }
                 P.tiled_nnz += rp[r + 1] - rp[r];
             }

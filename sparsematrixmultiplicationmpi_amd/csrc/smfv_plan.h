@@ -219,13 +219,14 @@ double parts_footprint(int m, int n, const int *row_ptr, const int *col_idx, con
 // of them, addressed by u16 image offsets.  Per tile, rows sorted by
 // decreasing length are dealt TW at a time to the 8 compute waves (wave
 // groups g and 7 - g share a SIMD); a wave's rows run in lockstep batches of
-// 8 entries, its teams' batches interleaved (offsets of batch b of team k in
-// the 16-byte chunk base + b TW + k: 8 u16; value pair q of that batch in
-// chunk vbase + (4 b + q) TW + k), so one wave read of 16 B per lane touches
+// WSN_B = 4 entries, its teams' batches interleaved (offsets of batch b of
+// team k in the 8-byte chunk base + b TW + k: 4 u16; value pair q of that
+// batch in chunk vbase + (2 b + q) TW + k), so one wave read per lane touches
 // TW consecutive chunks.  A row's entries past its length in its last batch
 // are pads: the zero image row and value -0.0 (summed: +-0 changes nothing).
 // ---------------------------------------------------------------------------
 constexpr int WSN_LW = 8;        // loader waves (8 compute + 8 loader = 1024 lanes)
+constexpr int WSN_B = 4;         // (r5) entries per batch (was 8: rows padded to 4, not 8 -- 21 % fewer entries)
 constexpr int WSN_GWORDS = 1024 + 96;  // global record: union ids [0, 1024), then 6 x 16 header words
 constexpr int WSN_G_NOFF = 1024, WSN_G_TN = 1040, WSN_G_NU = 1056, WSN_G_VOFF = 1072, WSN_G_TNV = 1088;
 struct WsnGeom {
