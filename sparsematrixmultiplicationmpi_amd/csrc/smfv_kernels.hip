@@ -1150,9 +1150,13 @@ __global__ __launch_bounds__(1024, 1) void k_rows_wsn(WsXcd xr, const int *__res
             const int row = word & 0xFFFFFF, nbat = (int)((unsigned)word >> 24);
             // (r5) batches of WSN_B = 4 entries: 4 u16 image rows in one 8-byte
             // read, two value pairs; X of batch b + 1 is read before batch b
-            // is summed
+            // is summed.  Batches hold only the teams still running (a prefix
+            // of the wave, smfv_plan.h): their count n_b is the lanes of
+            // more than b batches, over TL -- a ballot among the lanes in
+            // the loop, wave-uniform (scalar)
             const u2 *Lq = reinterpret_cast<const u2 *>(mbase + L::M_L) + RR[R + 2 * wv] + k;
             const d2 *Vq = reinterpret_cast<const d2 *>(mbase + L::M_V) + RR[R + 2 * wv + 1] + k;
+            auto nact = [&](int b) { return (int)__builtin_popcountll(__builtin_amdgcn_ballot_w64(nbat > b)) / TL; };
             d2 acc = {0.0, 0.0};
             auto rdx = [&](u2 w, d2 (&x)[4]) {
 #pragma unroll
@@ -1163,25 +1167,32 @@ __global__ __launch_bounds__(1024, 1) void k_rows_wsn(WsXcd xr, const int *__res
                 }
             };
             d2 xa[4], xb[4];
+            int n0 = nact(0), n1 = nact(1);  // teams in batches b, b + 1; Lq / Vq at batch b
             rdx(Lq[0], xa);
-            u2 on = Lq[min(1, nbat - 1) * TW];
+            u2 on = Lq[nbat > 1 ? n0 : 0];  // (a re-read of batch b when there is no next)
             for (int b = 0; b < nbat; b += 2) {
                 // batch b in xa; batch b + 1's reads go out first
-                d2 v0 = Vq[(2 * b) * TW], v1 = Vq[(2 * b + 1) * TW];
+                d2 v0 = Vq[0], v1 = Vq[n0];
                 rdx(on, xb);
-                on = Lq[min(b + 2, nbat - 1) * TW];
+                const int n2 = nact(b + 2);
+                on = Lq[nbat > b + 2 ? n0 + n1 : 0];
                 acc = madd(acc, v0.x, xa[0]);
                 acc = madd(acc, v0.y, xa[1]);
                 acc = madd(acc, v1.x, xa[2]);
                 acc = madd(acc, v1.y, xa[3]);
                 if (b + 1 < nbat) {
-                    v0 = Vq[(2 * b + 2) * TW], v1 = Vq[(2 * b + 3) * TW];
+                    v0 = Vq[2 * n0], v1 = Vq[2 * n0 + n1];
                     rdx(on, xa);
-                    on = Lq[min(b + 3, nbat - 1) * TW];
+                    const int n3 = nact(b + 3);
+                    on = Lq[nbat > b + 3 ? n0 + n1 + n2 : n0];
                     acc = madd(acc, v0.x, xb[0]);
                     acc = madd(acc, v0.y, xb[1]);
                     acc = madd(acc, v1.x, xb[2]);
                     acc = madd(acc, v1.y, xb[3]);
+                    Lq += n0 + n1;
+                    Vq += 2 * (n0 + n1);
+                    n0 = n2;
+                    n1 = n3;
                 }
             }
             __builtin_nontemporal_store(acc, reinterpret_cast<d2 *>(Y + (int64_t)row * ldy + 2 * tli));

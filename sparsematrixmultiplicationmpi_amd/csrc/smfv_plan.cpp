@@ -1198,6 +1198,18 @@ bool verify_wsn_plan(int m, int n, const int *rp, const int *ci, const WsnPlan &
             if (g[u] < 0 || g[u] >= std::max(n, 1) || (u >= nu && g[u] != 0)) return fail("union id out of range");
         for (int w = 0; w < 8; ++w) {
             const int lb = l[R + 2 * w], vb = l[R + 2 * w + 1];
+            // the kernel takes n_b (teams of more than b batches) from a ballot
+            // and places team k at c_b + k: the running teams must be a prefix
+            std::vector<int> nb_at, cum(1, 0);
+            for (int k = 0, prev = 255; k < TW; ++k) {
+                const int word = l[w * TW + k];
+                const int nbk = word == -1 ? 0 : (int)((unsigned)word >> 24);
+                if (nbk > prev) return fail("wave rows not in decreasing batch order");
+                prev = nbk;
+                if ((int)nb_at.size() < nbk) nb_at.resize((size_t)nbk, 0);
+                for (int b = 0; b < nbk; ++b) ++nb_at[(size_t)b];
+            }
+            for (int c : nb_at) cum.push_back(cum.back() + c);
             for (int k = 0; k < TW; ++k) {
                 const int word = l[w * TW + k];
                 if (word == -1) continue;
@@ -1209,10 +1221,12 @@ bool verify_wsn_plan(int m, int n, const int *rp, const int *ci, const WsnPlan &
                 for (int b = 0; b < nbat; ++b)
                     for (int e = 0; e < WSN_B; ++e) {
                         const int el = WSN_B * b + e;
-                        const int64_t le = (int64_t)noff + WSN_B * (int64_t)(lb + b * TW + k) + e;
+                        const int64_t le = (int64_t)noff + WSN_B * (int64_t)(lb + cum[(size_t)b] + k) + e;
                         const int64_t ve =
-                            (int64_t)voff + 2 * (int64_t)(vb + (WSN_B / 2 * b + e / 2) * TW + k) + e % 2;
-                        if (le >= noff + tn || ve >= voff + tnv) return fail("segment leaves its tile");
+                            (int64_t)voff +
+                            2 * (int64_t)(vb + 2 * cum[(size_t)b] + (e / 2) * nb_at[(size_t)b] + k) + e % 2;
+                        if (le < noff || le >= noff + tn || ve < voff || ve >= voff + tnv)
+                            return fail("segment leaves its tile");
                         if (el < rl) {
                             const int j = rp[r] + el, u = P.loff[(size_t)le];
                             if (P.tsrc[(size_t)ve] != j || u >= nu || g[u] != ci[j])
@@ -1260,10 +1274,10 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
             return la != lb ? la > lb : a < b;
         });
     };
-    auto layout = [&](const std::vector<int> &rows) {  // padded entries (rows sorted by decreasing length)
+    auto layout = [&](const std::vector<int> &rows) {  // entries with pads, trimmed per batch (16-byte multiple)
         int64_t e = 0;
-        for (size_t g = 0; g < rows.size(); g += (size_t)TW) e += (int64_t)nbat(rows[g]) * TW * WSN_B;
-        return e;
+        for (int r : rows) e += (int64_t)nbat(r) * WSN_B;
+        return (e + 7) & ~(int64_t)7;
     };
     std::vector<std::vector<int>> tiles, stack;
     const int np = (int)T.part_tile.size() - 1;
@@ -1334,28 +1348,35 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
         for (int s = 0; s < R; ++s) l[s] = -1;
         // wave group q (TW consecutive rows of the sorted list) -> wave w;
         // groups q and 7 - q share a SIMD (waves w and w + 4)
+        // (r5) per batch only the wave's teams still running (smfv_plan.h)
         int64_t chunk = 0;  // offset chunks so far (WSN_B entries each)
-        int lbase[8] = {}, vbase[8] = {}, wnb[8] = {};
-        for (int q = 0; q < 8 && (size_t)q * TW < Rw.size(); ++q) {
-            const int w = q < 4 ? q : 11 - q;
-            wnb[w] = nbat(Rw[(size_t)q * TW]);
-        }
-        int64_t vchunk = 0;
+        int lbase[8] = {}, vbase[8] = {};
         for (int w = 0; w < 8; ++w) {
+            const int q = w < 4 ? w : 11 - w;  // the wave's group
             lbase[w] = (int)chunk;
-            vbase[w] = (int)vchunk;
-            chunk += (int64_t)wnb[w] * TW;
-            vchunk += (int64_t)wnb[w] * (WSN_B / 2) * TW;
+            vbase[w] = (int)(WSN_B / 2 * chunk);
+            for (int k = 0; k < TW && (size_t)(q * TW + k) < Rw.size(); ++k) chunk += nbat(Rw[(size_t)(q * TW + k)]);
         }
+        std::vector<int> nb_at, cum;
         for (int q = 0; q < 8 && (size_t)q * TW < Rw.size(); ++q) {
             const int w = q < 4 ? q : 11 - q;
-            for (int k = 0; k < TW && (size_t)(q * TW + k) < Rw.size(); ++k) {
+            const int nt_q = (int)std::min<size_t>(TW, Rw.size() - (size_t)q * TW);
+            const int NB = nbat(Rw[(size_t)q * TW]);
+            nb_at.assign((size_t)NB, 0);
+            cum.assign((size_t)NB + 1, 0);
+            for (int k = 0; k < nt_q; ++k)
+                for (int b = 0; b < nbat(Rw[(size_t)(q * TW + k)]); ++b) ++nb_at[(size_t)b];
+            for (int b = 0; b < NB; ++b) cum[(size_t)b + 1] = cum[(size_t)b] + nb_at[(size_t)b];
+            for (int k = 0; k < nt_q; ++k) {
                 const int r = Rw[(size_t)(q * TW + k)];
                 l[w * TW + k] = r | (nbat(r) << 24);
                 for (int j = rp[r]; j < rp[r + 1]; ++j) {
                     const int el = j - rp[r], b = el / WSN_B, e = el % WSN_B;
-                    P.loff[(size_t)(noff + WSN_B * (int64_t)(lbase[w] + b * TW + k) + e)] = (uint16_t)pos[ci[j]];
-                    P.tsrc[(size_t)(noff + 2 * (int64_t)(vbase[w] + (WSN_B / 2 * b + e / 2) * TW + k) + e % 2)] = j;
+                    P.loff[(size_t)(noff + WSN_B * (int64_t)(lbase[w] + cum[(size_t)b] + k) + e)] =
+                        (uint16_t)pos[ci[j]];
+                    P.tsrc[(size_t)(noff +
+                                    2 * (int64_t)(vbase[w] + 2 * cum[(size_t)b] + (e / 2) * nb_at[(size_t)b] + k) +
+                                    e % 2)] = j;
                 }
                 P.tiled_nnz += rp[r + 1] - rp[r];
             }

@@ -219,11 +219,15 @@ double parts_footprint(int m, int n, const int *row_ptr, const int *col_idx, con
 // of them, addressed by u16 image offsets.  Per tile, rows sorted by
 // decreasing length are dealt TW at a time to the 8 compute waves (wave
 // groups g and 7 - g share a SIMD); a wave's rows run in lockstep batches of
-// WSN_B = 4 entries, its teams' batches interleaved (offsets of batch b of
-// team k in the 8-byte chunk base + b TW + k: 4 u16; value pair q of that
-// batch in chunk vbase + (2 b + q) TW + k), so one wave read per lane touches
-// TW consecutive chunks.  A row's entries past its length in its last batch
-// are pads: the zero image row and value -0.0 (summed: +-0 changes nothing).
+// WSN_B = 4 entries, its teams' batches interleaved and trimmed to the teams
+// still running: with n_b the wave's teams of more than b batches (a prefix,
+// rows being sorted) and c_b = n_0 + ... + n_{b-1}, the offsets of batch b of
+// team k sit in the 8-byte chunk base + c_b + k (4 u16) and value pair q of
+// that batch in the 16-byte chunk vbase + 2 c_b + q n_b + k, so one wave read
+// per lane touches n_b consecutive chunks and a wave's rows cost their own
+// batches, not its longest row's (the kernel counts n_b with a ballot).  A
+// row's entries past its length in its last batch are pads: the zero image
+// row and value -0.0 (summed: +-0 changes nothing).
 // ---------------------------------------------------------------------------
 constexpr int WSN_LW = 8;        // loader waves (8 compute + 8 loader = 1024 lanes)
 constexpr int WSN_B = 4;         // (r5) entries per batch (was 8: rows padded to 4, not 8 -- 21 % fewer entries)
