@@ -999,10 +999,14 @@ def test_narrow_team_tiles(gpu, K):
     offsets): bit-identical to the reference's order, into a padded Y (the
     padding stays NaN), with direct rows; and identical to the k_rows_ws
     NARROW form (tiled_kernel="ws", the A/B); on both cop20k stand-ins at
-    full size."""
+    full size and on short / empty rows beside long ones."""
+    from conftest import short_rows_band
     rng = np.random.default_rng(200 + K)
     mats = [smfv.gen_fem27(9000, 14, 14, 0.83, K), smfv.gen_random_rows(7000, 6000, 16, 2.0, 1500, K),
-            smfv.cop20k_surrogate(), smfv.inputs.cop20k_irregular_surrogate()]
+            smfv.cop20k_surrogate(), smfv.inputs.cop20k_irregular_surrogate(),
+            # (r5) trimmed batches: rows of 0-7 entries beside 30-60 (empty rows,
+            # every length residue), and a tile with empty team slots
+            short_rows_band(6000, 31 + K), short_rows_band(77, 5 + K, long_every=9)]
     for A in mats:
         X = rng.uniform(-1, 1, (A.numCols, 32))
         dA = smfv.DeviceCSR(A, gpu)

@@ -673,8 +673,8 @@ def test_narrow_team_plan_on_host():
     """(r5) The k_rows_wsn plan of a 4 / 8-column window (a ColumnWise rank's
     panel) is built and verified on the host (its reads replayed): every row
     once, in CSR order, pads on the zero image row; on the cop20k stand-in it
-    runs well under half the units of k_rows_ws's 2,011 tiles, and a row too
-    long for a tile becomes direct."""
+    runs well under half the units of k_rows_ws's 2,011 tiles with < 8 %
+    padded entries, and a row too long for a tile becomes direct."""
     ip = ctypes.POINTER(ctypes.c_int)
 
     def wsn(A, kw, r0=0, r1=None):
@@ -686,7 +686,9 @@ def test_narrow_team_plan_on_host():
     for kw, rows in ((4, 256), (8, 128)):
         tiles, union, reuse, direct, most, entries = wsn(A, kw)
         assert 0 < tiles < 2011 * 0.6 and direct == 0 and most <= rows and reuse > 6.0, (kw, tiles, reuse)
-        assert entries >= A.nnz
+        # (r5) batches of 4 trimmed to the running teams: 2.80 M entries for
+        # 2.62 M non-zeros (3.54 M with untrimmed batches of 8)
+        assert A.nnz <= entries <= 1.08 * A.nnz, (kw, entries)
     P = smfv.gen_random_rows(5000, 5000, 12, 2.0, 5000, 3)  # a few very long rows
     tiles, union, reuse, direct, most, entries = wsn(P, 4)
     assert tiles > 0 and direct >= 1
