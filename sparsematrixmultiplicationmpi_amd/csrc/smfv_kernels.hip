@@ -1078,21 +1078,35 @@ __global__ __launch_bounds__(1024, 1) void k_rows_wsn(WsXcd xr, const int *__res
         if (wl == 0 && lane < 2 * (XROW / 16))  // the zero image row of both X slots
             reinterpret_cast<d2 *>(lds + (lane / (XROW / 16)) * L::XSLOT + UCAP * XROW)[lane % (XROW / 16)] =
                 d2{0.0, 0.0};
+        // (r5) a tile's record is read in two steps a unit apart: its header
+        // (entry ranges, union size nu) two units ahead of its staging, its
+        // union ids one unit ahead and only the first nu of them (a tile
+        // stages ~420 of the 1,024 slots at K/p = 4), so no load waits on
+        // another inside a unit
         int uid[L::PPW];
-        int noff, tn, nu, voff, tnv;
+        int noff, tn, nu, voff, tnv;       // the tile staged next
+        int noff2, tn2, nu2, voff2, tnv2;  // the one after it
         const unsigned ldxb = (unsigned)(ldx * 8);
-        auto fetch_record = [&](int t) {
+        auto fetch_ids = [&](int t, int n_u) {
             const int *Gr = grec + (int64_t)t * WSN_GWORDS;
 #pragma unroll
             for (int i = 0; i < L::PPW; ++i) {
                 const int piece = wl + WSN_LW * i;
-                uid[i] = piece < L::XPIECES ? Gr[L::RP * piece + lane / TL] : 0;
+                uid[i] = piece < L::XPIECES && L::RP * piece + lane / TL < n_u ? Gr[L::RP * piece + lane / TL] : 0;
             }
-            noff = Gr[WSN_G_NOFF + (lane & 15)];
-            tn = Gr[WSN_G_TN + (lane & 15)];
-            nu = Gr[WSN_G_NU + (lane & 15)];
-            voff = Gr[WSN_G_VOFF + (lane & 15)];
-            tnv = Gr[WSN_G_TNV + (lane & 15)];
+        };
+        auto fetch_header = [&](int t) {
+            const int *Gr = grec + (int64_t)t * WSN_GWORDS;
+            noff2 = Gr[WSN_G_NOFF + (lane & 15)];
+            tn2 = Gr[WSN_G_TN + (lane & 15)];
+            nu2 = Gr[WSN_G_NU + (lane & 15)];
+            voff2 = Gr[WSN_G_VOFF + (lane & 15)];
+            tnv2 = Gr[WSN_G_TNV + (lane & 15)];
+        };
+        auto advance = [&](int t) {  // the header after next becomes next; its ids and the next header go out
+            noff = noff2, tn = tn2, nu = nu2, voff = voff2, tnv = tnv2;
+            fetch_ids(t, nu);
+            fetch_header(min(t + nb, tlast));
         };
         auto stage = [&](int t, int slot) {
 #pragma unroll
@@ -1116,16 +1130,19 @@ __global__ __launch_bounds__(1024, 1) void k_rows_wsn(WsXcd xr, const int *__res
                 if (wl == WSN_LW - 1 - k && 16 * lane + 1024 * k < L::RECB)
                     dma16s<true>(lrec + (int64_t)t * L::G.lwords(), 1024u * k + 16u * lane, mb + L::M_R + k * 1024);
         };
-        fetch_record(t0);
+        fetch_header(t0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        advance(t0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         stage(t0, 0);
-        fetch_record(min(t0 + nb, tlast));
+        advance(min(t0 + nb, tlast));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         barrier_lds();
         for (int u = 0; u < cnt; ++u) {
             if (u + 1 < cnt) {
                 const int t = t0 + (u + 1) * nb;
                 stage(t, (u + 1) & 1);
-                fetch_record(min(t + nb, tlast));
+                advance(min(t + nb, tlast));
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // unit u + 1 has landed
             barrier_lds();
