@@ -1082,7 +1082,8 @@ __global__ __launch_bounds__(1024, 1) void k_rows_wsn(WsXcd xr, const int *__res
         // (entry ranges, union size nu) two units ahead of its staging, its
         // union ids one unit ahead and only the first nu of them (a tile
         // stages ~420 of the 1,024 slots at K/p = 4), so no load waits on
-        // another inside a unit
+        // another inside a unit; the first tile reads every slot (no extra
+        // round trip before the pipeline fills)
         int uid[L::PPW];
         int noff, tn, nu, voff, tnv;       // the tile staged next
         int noff2, tn2, nu2, voff2, tnv2;  // the one after it
@@ -1095,14 +1096,15 @@ __global__ __launch_bounds__(1024, 1) void k_rows_wsn(WsXcd xr, const int *__res
                 uid[i] = piece < L::XPIECES && L::RP * piece + lane / TL < n_u ? Gr[L::RP * piece + lane / TL] : 0;
             }
         };
-        auto fetch_header = [&](int t) {
+        auto load_header = [&](int t, int &no, int &n, int &u, int &vo, int &nv) {
             const int *Gr = grec + (int64_t)t * WSN_GWORDS;
-            noff2 = Gr[WSN_G_NOFF + (lane & 15)];
-            tn2 = Gr[WSN_G_TN + (lane & 15)];
-            nu2 = Gr[WSN_G_NU + (lane & 15)];
-            voff2 = Gr[WSN_G_VOFF + (lane & 15)];
-            tnv2 = Gr[WSN_G_TNV + (lane & 15)];
+            no = Gr[WSN_G_NOFF + (lane & 15)];
+            n = Gr[WSN_G_TN + (lane & 15)];
+            u = Gr[WSN_G_NU + (lane & 15)];
+            vo = Gr[WSN_G_VOFF + (lane & 15)];
+            nv = Gr[WSN_G_TNV + (lane & 15)];
         };
+        auto fetch_header = [&](int t) { load_header(t, noff2, tn2, nu2, voff2, tnv2); };
         auto advance = [&](int t) {  // the header after next becomes next; its ids and the next header go out
             noff = noff2, tn = tn2, nu = nu2, voff = voff2, tnv = tnv2;
             fetch_ids(t, nu);
@@ -1130,9 +1132,11 @@ __global__ __launch_bounds__(1024, 1) void k_rows_wsn(WsXcd xr, const int *__res
                 if (wl == WSN_LW - 1 - k && 16 * lane + 1024 * k < L::RECB)
                     dma16s<true>(lrec + (int64_t)t * L::G.lwords(), 1024u * k + 16u * lane, mb + L::M_R + k * 1024);
         };
-        fetch_header(t0);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        advance(t0);
+        // the first tile in one round trip: its header and every id slot
+        // together, the second tile's header beside them
+        load_header(t0, noff, tn, nu, voff, tnv);
+        fetch_ids(t0, L::UCAP + 1);
+        fetch_header(min(t0 + nb, tlast));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         stage(t0, 0);
         advance(min(t0 + nb, tlast));
