@@ -1259,11 +1259,11 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
     TileCaps caps = caps_in;
     caps.ucap = G.ucap;
     caps.maxrows = R;
-    caps.pad = 8;
+    caps.pad = WSN_B;
     // the analysis counts each row padded to 8; the layout pads a wave's rows
     // to its longest, so the analysis aims below the cap and the layout
     // checks the real figure (splitting a tile that still overflows)
-    caps.ncap = G.ncap * frac_num / frac_den;
+    caps.ncap = G.ncap * frac_num / frac_den - 8;
     TileAnalysis T;
     analyse_tiles(m, n, rp, ci, T, caps);
 
@@ -1409,7 +1409,13 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
 bool build_wsn_plan(int m, int n, const int *rp, const int *ci, int kw, WsnPlan &P, std::string *err,
                     const TileCaps &caps)
 {
-    static constexpr int fr[4][2] = {{3, 4}, {13, 16}, {7, 8}, {9, 10}};
+    static constexpr int fr[6][2] = {{3, 4}, {13, 16}, {7, 8}, {9, 10}, {15, 16}, {1, 1}};
+    const int nbk = std::max(1, caps.xcd_blocks);
+    auto rounds = [&](const WsnPlan &W) {  // units on the busiest blocks
+        int r = 0;
+        for (int x = 0; x < 8; ++x) r = std::max(r, (W.xcd[x + 1] - W.xcd[x] + nbk - 1) / nbk);
+        return r;
+    };
     bool any = false;
     for (const auto &f : fr) {
         WsnPlan Q;
@@ -1418,7 +1424,12 @@ bool build_wsn_plan(int m, int n, const int *rp, const int *ci, int kw, WsnPlan 
             if (err && !any) *err = e;
             continue;
         }
-        if (!any || Q.ntiles < P.ntiles || (Q.ntiles == P.ntiles && Q.union_rows < P.union_rows)) P = std::move(Q);
+        if (getenv("WSN_DEBUG")) fprintf(stderr, "wsn frac %d/%d: %d tiles, %lld union rows\n", f[0], f[1], Q.ntiles, (long long)Q.union_rows);
+        static const bool few = getenv("SMFV_WSN_FEW") && *getenv("SMFV_WSN_FEW") == '1';  // (A/B)
+        const bool more = few ? Q.ntiles < P.ntiles : Q.ntiles > P.ntiles;
+        const bool better = !any || rounds(Q) < rounds(P) ||
+                            (rounds(Q) == rounds(P) && (more || (Q.ntiles == P.ntiles && Q.union_rows < P.union_rows)));
+        if (better) P = std::move(Q);
         any = true;
     }
     return any;
