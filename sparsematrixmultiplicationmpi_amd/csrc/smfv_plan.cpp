@@ -1260,9 +1260,10 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
     caps.ucap = G.ucap;
     caps.maxrows = R;
     caps.pad = WSN_B;
-    // the analysis counts each row padded to 8; the layout pads a wave's rows
-    // to its longest, so the analysis aims below the cap and the layout
-    // checks the real figure (splitting a tile that still overflows)
+    // the analysis counts each row padded to WSN_B entries, the layout's own
+    // figure for the trimmed batches but for its 16-byte round-up (hence the
+    // 8 entries of room); the layout checks the real figure (splitting a tile
+    // that still overflows, e.g. one holding empty rows, which own a batch)
     caps.ncap = G.ncap * frac_num / frac_den - 8;
     TileAnalysis T;
     analyse_tiles(m, n, rp, ci, T, caps);
@@ -1401,11 +1402,13 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
 }  // namespace
 
 // The analysis aims at a fraction of the entry cap (it counts each row
-// padded to 8, the layout pads a wave's rows to its longest, and a tile that
-// still overflows is split in halves); the best fraction depends on the
-// row-length spread (cop20k stand-ins, tiles at 3/4 .. 9/10: 884-975 /
-// 1,095-1,294 stencil, 1,110-1,319 / 1,449-1,612 irregular at K = 4 / 8),
-// so four are built and the plan with the fewest tiles is kept.
+// padded to 4, as the layout's trimmed batches do; a tile that still
+// overflows is split in halves).  The kernel's time follows the rounds of
+// units on its busiest blocks (32 per XCD), so six fractions (3/4 .. 1) are
+// built and the plan with the fewest rounds is kept, then the fewest tiles
+// (r5, cop20k stand-ins: 705 / 968 stencil, 762 / 1,184 irregular tiles at
+// K = 4 / 8: 3 / 4 / 3 / 5 rounds; ColumnWise rank panels 4-10 % faster
+// than the previous 819 / 1,084 / 870 / 1,286, profiles/r05/wsn/README.md).
 bool build_wsn_plan(int m, int n, const int *rp, const int *ci, int kw, WsnPlan &P, std::string *err,
                     const TileCaps &caps)
 {
@@ -1424,11 +1427,9 @@ bool build_wsn_plan(int m, int n, const int *rp, const int *ci, int kw, WsnPlan 
             if (err && !any) *err = e;
             continue;
         }
-        if (getenv("WSN_DEBUG")) fprintf(stderr, "wsn frac %d/%d: %d tiles, %lld union rows\n", f[0], f[1], Q.ntiles, (long long)Q.union_rows);
-        static const bool few = getenv("SMFV_WSN_FEW") && *getenv("SMFV_WSN_FEW") == '1';  // (A/B)
-        const bool more = few ? Q.ntiles < P.ntiles : Q.ntiles > P.ntiles;
         const bool better = !any || rounds(Q) < rounds(P) ||
-                            (rounds(Q) == rounds(P) && (more || (Q.ntiles == P.ntiles && Q.union_rows < P.union_rows)));
+                            (rounds(Q) == rounds(P) &&
+                             (Q.ntiles < P.ntiles || (Q.ntiles == P.ntiles && Q.union_rows < P.union_rows)));
         if (better) P = std::move(Q);
         any = true;
     }

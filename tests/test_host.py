@@ -659,9 +659,8 @@ def test_ws_kernels_register_budget(tmp_path):
         vgpr = int(re.search(r"\.vgpr_count:\s+(\d+)", blk).group(1))
         spill = int(re.search(r"\.vgpr_spill_count:\s+(\d+)", blk).group(1))
         geo = re.search(r"k_rows_ws(?:_live)?ILi(\d+)ELi(\d+)E", name)
-        if geo is None:  # (r5) k_rows_wsn, k_rows_ws_split: one 1024-lane block per CU
-            assert ("k_rows_wsn" in name or "k_rows_ws_split" in name) and vgpr <= 128 and spill == 0, \
-                (name, vgpr, spill)
+        if geo is None:  # (r5) k_rows_wsn: one 1024-lane block per CU
+            assert "k_rows_wsn" in name and vgpr <= 128 and spill == 0, (name, vgpr, spill)
             continue
         cw, lw = map(int, geo.groups())
         waves_per_simd = 4 if (cw, lw) in ((8, 8), (4, 4)) else 3
