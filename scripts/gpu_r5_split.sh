@@ -4,6 +4,8 @@
 # of the tiled kernels with SPLIT on, then an A/B on one box, alternating per
 # config: this build (split off: the refactored k_rows_ws), split on, and the
 # previous build (libsmfv_ab.so).
+# (Kept as the record of that run: the split kernel was measured 12-18 % slower and
+# never committed, profiles/r05/wsn/README.md; without it both legs run k_rows_ws.)
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 out=gpurun_out/split
 mkdir -p $out
