@@ -1318,28 +1318,6 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
             P.xcd[x] = (int)std::max<int64_t>(std::min<int64_t>(P.xcd[x], P.xcd[x - 1] + cap),
                                               std::max<int64_t>(N - cap * (8 - x), P.xcd[x - 1]));
     }
-    // (A/B, SMFV_WSN_ENDS=1) an XCD's first and last rounds take its smallest
-    // tiles (the pipeline's fill and drain), the middle rounds the largest
-    static const bool ends = getenv("SMFV_WSN_ENDS") && *getenv("SMFV_WSN_ENDS") == '1';
-    if (ends) {
-        const int nbk = std::max(1, caps.xcd_blocks);
-        for (int x = 0; x < 8; ++x) {
-            const int a = P.xcd[x], b = P.xcd[x + 1];
-            if (b - a <= nbk) continue;
-            std::vector<std::vector<int>> part(tiles.begin() + a, tiles.begin() + b);
-            std::stable_sort(part.begin(), part.end(),
-                             [&](const std::vector<int> &u, const std::vector<int> &v) { return layout(u) < layout(v); });
-            const int n = b - a, last = (n - 1) / nbk * nbk;  // first slot of the last round
-            const int nlast = n - last;
-            // smallest nbk -> round 0, next nlast -> the last round, the rest (largest) between
-            std::vector<std::vector<int>> out((size_t)n);
-            int k = 0;
-            for (int i = 0; i < nbk; ++i) out[(size_t)i] = std::move(part[(size_t)k++]);
-            for (int i = 0; i < nlast; ++i) out[(size_t)(last + i)] = std::move(part[(size_t)k++]);
-            for (int i = nbk; i < last; ++i) out[(size_t)i] = std::move(part[(size_t)k++]);
-            std::move(out.begin(), out.end(), tiles.begin() + a);
-        }
-    }
     const int nt = (int)N;
     std::vector<int64_t> toff((size_t)nt + 1, 0);
     for (int t = 0; t < nt; ++t) toff[(size_t)t + 1] = toff[(size_t)t] + layout(tiles[(size_t)t]);
