@@ -30,10 +30,12 @@ it, the matrix is the labelled surrogate of inputs.cop20k_surrogate() (same
 m = 121,192, nnz = 2,624,346 vs 2,624,331, symmetric 27-point-stencil
 pattern).  X is the reference's fat vector (rand()%100+1, glibc seed 1).
 
-The cpu_baseline leg (rank 0, N = 1 only, before the GPU is touched) times
-the REFERENCE's own RowWise MPI kernel (oracle/_ref/ref_driver, its sources
-compiled unmodified) under mpiexec on the host cores, as SC/main.cpp:161-163
-times it; without that binary it falls back to the oracle's C port.
+The cpu_baseline leg (rank 0, before the GPU is touched; r6: at every N,
+the other ranks waiting in the rendezvous) times the REFERENCE's own RowWise
+MPI kernel (oracle/_ref/ref_driver, its sources compiled unmodified) under
+mpiexec on the host cores, as SC/main.cpp:161-163 times it -- 16 ranks at
+N = 1 (with a 1-16 sweep), 16 * N ranks beside an N-GPU line; without that
+binary it falls back to the oracle's C port.
 """
 from __future__ import annotations
 
@@ -100,6 +102,14 @@ def measured_traffic(config: str, kernel: str):
     if not e or kernel.split("<")[0] not in (e.get("kernel") or ""):
         return None, None
     return e["traffic_bytes_per_launch"], e["source"]
+
+
+def measured_rank_traffic(config: str, p: int, rank: int, kernel: str):
+    """(r6) Per-launch HBM bytes of rank `rank`'s plan of the p-rank
+    decomposition (profiles/pmc_traffic.json key '<config>@p<p>r<rank>',
+    from a PMC run of `bench.py --rank-plans p --rank-only rank`: the same
+    rank plan smfv_dist_plan_create gives that rank)."""
+    return measured_traffic(f"{config}@p{p}r{rank}", kernel)
 
 
 def kernel_label(variant: str, K: int, plan_stats: dict, x_bytes: int = 0) -> str:
@@ -184,15 +194,26 @@ def _ref_run(A, K: int, tag: str, cores: int, binary: str, reps: int, timeout: f
     return float(mt.group(1)) if mt else None
 
 
+def cpu_ranks(world: int) -> int:
+    """MPI ranks of the CPU baseline beside an N-GPU line: 16 per GPU (the
+    box's CPU share of one GPU), capped at the CPUs this process may use
+    when N > 1 (N = 1 keeps the 16-rank point and its 1-16 sweep)."""
+    if world <= 1:
+        return 16
+    return max(1, min(16 * world, len(os.sched_getaffinity(0))))
+
+
 def cpu_baseline(A, K: int, variant: str, sample: str | None = None, budget_s: float = 20.0,
-                 sweep_ranks: bool = True) -> dict:
+                 sweep_ranks: bool = True, ranks: int = 16) -> dict:
     """The reference's own kernel (its sources compiled unmodified, g++ -O3,
     oracle/_ref/ref_driver) under mpiexec on this box's host cores: the
     16-rank rate (the box's CPU share per GPU) is `value`;
     `sweep_GFLOPs_by_ranks` holds 1/2/4/8/16 ranks and `O0_GFLOPs` the
     16-rank rate of the reference's documented unoptimised compile
     (README.md:29).  `sample` labels a bounded stand-in input
-    (configs 4-5).  Without the binary: the oracle's C port, one thread."""
+    (configs 4-5).  (r6) `ranks` != 16 (an N-GPU line: 16 * N, cpu_ranks)
+    times that many ranks as `value`, with the 16-rank point beside it, and
+    no sweep.  Without the binary: the oracle's C port, one thread."""
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
     ref0 = ref + "_O0"
     flops = 2.0 * A.nnz * K
@@ -205,11 +226,18 @@ def cpu_baseline(A, K: int, variant: str, sample: str | None = None, budget_s: f
         # SURVEY 8(d) also asks for -n nproc: run last, capped in time (over
         # the share it oversubscribes the 16 CPUs; its rate is reported, not used)
         nproc = os.cpu_count() or 16
-        counts = [1] if tag == "S" else ([1, 2, 4, 8, 16] if sweep_ranks else [16])
+        if tag == "S":
+            counts = [1]
+        elif ranks != 16:
+            sweep_ranks = False
+            counts = sorted({min(16, ranks), ranks})
+        else:
+            counts = [1, 2, 4, 8, 16] if sweep_ranks else [16]
+        many = len(counts) > 1
         sweep = {}
         for c in counts:
             # the reported point (the top rank count): median of 10 calls
-            t = _ref_run(A, K, tag, c, ref, 10 if c == counts[-1] and sweep_ranks else 3, budget_s * 6)
+            t = _ref_run(A, K, tag, c, ref, 10 if c == counts[-1] and many else 3, budget_s * 6)
             if t:
                 sweep[str(c)] = round(flops / t / 1e9, 4)
         nproc_point = None
@@ -227,8 +255,9 @@ def cpu_baseline(A, K: int, variant: str, sample: str | None = None, budget_s: f
                     "binding": "MPICH hydra " + " ".join(MPI_BIND) + " (one rank per core), -launcher fork",
                     "nproc_point": nproc_point,
                     "sample": f"{what}, reference {name} (SC sources, g++ -O3) under MPICH mpiexec -n {top}, "
-                              f"median of {10 if sweep_ranks else 3} calls incl. gather + FatVector rebuild"
-                              f"{'; 1/2/4/8/16-rank sweep and the -O0 build beside it' if sweep_ranks else ''}; "
+                              f"median of {10 if many else 3} calls incl. gather + FatVector rebuild"
+                              f"{'; 1/2/4/8/16-rank sweep and the -O0 build beside it' if sweep_ranks else ''}"
+                              f"{'; the 16-rank point (one GPU share) beside it' if many and not sweep_ranks else ''}; "
                               f"wall {time.time() - t0:.1f}s",
                     "seconds_per_call": flops / (sweep[top] * 1e9),
                     "sweep_GFLOPs_by_ranks": sweep,
@@ -401,22 +430,23 @@ class Deadline:
         self.timer = None
         self.phase = None
 
-    def enter(self, phase: str) -> None:
+    def enter(self, phase: str, seconds: float | None = None) -> None:
         import threading
         self.cancel()
         self.phase = phase
         if self.seconds <= 0:
             return
+        limit = self.seconds if seconds is None else seconds
         t0 = time.time()
 
         def expire():
             print(json.dumps({"metric": self.metric, "value": None, "unit": "GFLOP/s", "n_gpus": self.world,
-                              "error": f"rank {self.rank}: phase '{phase}' exceeded its {self.seconds:.0f} s "
+                              "error": f"rank {self.rank}: phase '{phase}' exceeded its {limit:.0f} s "
                                        f"deadline ({time.time() - t0:.0f} s)", "rank": self.rank}), flush=True)
             print(f"[bench] rank {self.rank}: deadline in phase {phase}; exiting with status 4",
                   file=sys.stderr, flush=True)
             os._exit(4)
-        self.timer = threading.Timer(self.seconds, expire)
+        self.timer = threading.Timer(limit, expire)
         self.timer.daemon = True
         self.timer.start()
 
@@ -484,6 +514,33 @@ def _graph_or_eager(step, steps: int, world: int):
     return _timed_events(run, world) / steps, "eager launches"
 
 
+CPU_BASELINE_WAIT_S = 900.0  # the other ranks' wait while rank 0 times the CPU baseline (N > 1)
+
+
+def rank0_cpu_baseline(args, world: int, rank: int, dl, fn):
+    """(r6) The CPU/MPI baseline beside EVERY line, N > 1 included
+    (north_star: GFLOP/s at 1/2/4/8 GPUs alongside the CPU/MPI baseline):
+    rank 0 runs fn() -- the reference's kernel under mpiexec on 16 ranks per
+    GPU (cpu_ranks) -- before anything touches a GPU, while the other ranks
+    wait for it in the process-group rendezvous (under a longer deadline).
+    Returns the baseline dict on rank 0, None elsewhere."""
+    if args.no_cpu_baseline:
+        return None
+    if rank != 0:
+        if world > 1 and dl is not None:
+            dl.enter("waiting for rank 0's CPU baseline (process-group rendezvous)",
+                     seconds=args.phase_timeout + CPU_BASELINE_WAIT_S)
+        return None
+    if dl is not None:
+        dl.enter("CPU baseline (reference kernel under mpiexec, before the GPU is touched)",
+                 seconds=args.phase_timeout + CPU_BASELINE_WAIT_S)
+    cpu = fn()
+    if cpu is not None and world > 1:
+        cpu["note_n_gpus"] = (f"beside the {world}-GPU line: {cpu.get('cores')} MPI ranks = 16 per GPU "
+                              f"(capped at the {len(os.sched_getaffinity(0))} CPUs this process may use)")
+    return cpu
+
+
 def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
     """BASELINE config 5: synthetic m x m (m = 80M), 16 uniform-random
     columns per row (splitmix64, seed 42), X = hash integers 1..100 (seed 43).
@@ -504,13 +561,15 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
 
     m = n = args.rows or SYN80M_ROWS
     dl = Deadline(args.phase_timeout, rank, world, metric_for("syn80m_k32", K, "ROWWISE"))
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+
+    def _cpu():
         # before the GPU is touched; the reference's int32 m*K indexing cannot
         # hold 80M x 32, so a bounded 1M x 1M instance of the same generator
         S = inputs.gen_random_rows(1_000_000, 1_000_000, 16.0, 0.0, 16, 42)
-        cpu = cpu_baseline(S, K, "ROWWISE", sample=f"bounded sample: 1M x 1M instance of the same generator "
-                                                   f"(16 uniform-random columns per row), K={K}", sweep_ranks=False)
+        return cpu_baseline(S, K, "ROWWISE", sample=f"bounded sample: 1M x 1M instance of the same generator "
+                                                    f"(16 uniform-random columns per row), K={K}", sweep_ranks=False,
+                            ranks=cpu_ranks(world))
+    cpu = rank0_cpu_baseline(args, world, rank, dl, _cpu)
     first, last, _, _ = D.exchange_plan(smfv.Variant.ROWWISE, m, 0, None, K, world)
     r0, r1 = int(first[rank]), int(last[rank]) + 1
     t0 = time.time()
@@ -644,6 +703,9 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     A, label = build_matrix(kind, args.mtx)
     m, n, nnz = A.numRows, A.numCols, A.nnz
     dl = Deadline(args.phase_timeout, rank, world, metric_for(args.config, K, variant))
+    cpu = rank0_cpu_baseline(args, world, rank, dl,
+                             lambda: cpu_baseline(A, K, variant, sweep_ranks=False, ranks=cpu_ranks(world)))
+    args.cpu_baseline_done = cpu  # (a replicas fallback reports it: the GPU is touched below)
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
@@ -750,6 +812,11 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     else:
         loc_bytes = prob_bytes // world
     keys = list(beside)
+    # (r6) every rank's local time and bytes: the roofline is the slowest rank's
+    per_rank = torch.zeros(2 * world, dtype=torch.float64)
+    per_rank[2 * rank], per_rank[2 * rank + 1] = ms_loc, float(loc_bytes)
+    if world > 1:
+        dist.all_reduce(per_rank)
     vals = [ms_step, ms_loc, ms_rep, float(loc_bytes) / max(ms_loc, 1e-9), 0.0 if ok else 1.0]
     for key in keys:
         vals += [beside[key][0], beside[key][1]]
@@ -764,7 +831,11 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     flops = 2.0 * nnz * K
     st = plans["value"].stats()
     if rank == 0:
-        loc_gbps = float(tmin[3]) * 1e-6  # the slowest rank's local bytes / its local time (GB/s)
+        pr = per_rank.tolist()
+        slow = max(range(world), key=lambda r: pr[2 * r])
+        s_ms, s_bytes = pr[2 * slow], int(pr[2 * slow + 1])
+        loc_gbps = s_bytes / (s_ms * 1e-3) / 1e9  # the slowest rank's local bytes / its local time (GB/s)
+        traffic, traffic_src = measured_rank_traffic(args.config, world, slow, kernel_label(variant, K, st, 8 * n * K))
         others = {}
         for i, key in enumerate(keys):
             ms_k, ms_kl = tl[5 + 2 * i], tl[6 + 2 * i]
@@ -786,11 +857,16 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
                                       f"({'work-balanced row blocks' if rows and args.partition == 'balanced' else 'SC partition formulas'}), "
                                       "A and X replicated, Y all-gathered", "copies_rotated": ncopies},
             "roofline": {"bound": "hbm", "achieved": round(loc_gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(loc_gbps / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "frac": round(loc_gbps / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": kernel_label(variant, K, st, 8 * n * K),
-                         "algorithmic_bytes_per_launch": int(loc_bytes),
-                         "avg_launch_ms": round(ms_loc, 6),
-                         "timing": f"rank-local kernel alone ({how_loc}), slowest rank"},
+                         "rank": slow,
+                         "algorithmic_bytes_per_launch": s_bytes,
+                         "avg_launch_ms": round(s_ms, 6),
+                         "per_rank": [{"rank": r, "local_ms": round(pr[2 * r], 6),
+                                       "algorithmic_bytes": int(pr[2 * r + 1])} for r in range(world)],
+                         "timing": f"rank-local kernel alone ({how_loc}), slowest rank; traffic: that rank's "
+                                   "plan under rocprofv3 PMC on one GPU (bench.py --rank-plans N --rank-only r)"},
             "rank_local_ms": round(ms_loc, 6),
             "exchange_ms": round(ms_step - ms_loc, 6),
             "exchange_ms_gather_to_root": round(others["gather_to_root"]["exchange_ms"], 6),
@@ -809,7 +885,7 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
             "replicas": {"note": "every rank its own whole problem, no collective (weak scaling)",
                          "ms_per_step": round(ms_rep, 6),
                          "value_GFLOPs": round(world * flops / (ms_rep * 1e-3) / 1e9, 3)},
-            "cpu_baseline": None,
+            "cpu_baseline": cpu,
         }
         print(json.dumps(out))
     del copies, reps, plans
@@ -855,17 +931,20 @@ def bench_rank_plans(args, kind: str, K: int, variant: str) -> None:
     chunks = args.rank_chunks if rowwise else 1
     part = args.partition if rowwise else "reference"
     copies = []
+    # (r6) --rank-only r: rank r's plan alone (a PMC run of that rank's kernel)
+    sel = [args.rank_only] if 0 <= args.rank_only < p else list(range(p))
     for c in range(ncopies):
         dA = smfv.DeviceCSR(A, dev)
         dX = torch.from_numpy(X_host).to(dev)
         dY = torch.zeros((m, K), dtype=torch.float64, device=dev)
         plans = [D.DistPlan(None, V, dA, K, to_all=False, rank=(r, p), tiles=args.tiles,
-                            tiled_kernel=args.tiled_kernel, partition=part, chunks=chunks) for r in range(p)]
+                            tiled_kernel=args.tiled_kernel, partition=part, chunks=chunks) if r in sel else None
+                 for r in range(p)]
         copies.append((plans, dX, dY))
     torch.cuda.synchronize()
-    first, last, off, cnt = copies[0][0][0].partition()  # the plans' own partition
+    first, last, off, cnt = copies[0][0][sel[0]].partition()  # the plans' own partition
     ranks = []
-    for r in range(p):
+    for r in sel:
         def step(i, r=r):
             plans, dX, dY = copies[i % ncopies]
             plans[r].run_local(dX, dY)
@@ -892,6 +971,25 @@ def bench_rank_plans(args, kind: str, K: int, variant: str) -> None:
     plans, dX, dY = copies[0]
     dY.fill_(float("nan"))
     xbuf = None
+    if len(sel) < p:  # one rank: its ROWWISE rows against the same rows of the 1-GPU plan
+        ok, mabs = None, None
+        if rowwise:
+            r = sel[0]
+            r0, r1 = int(first[r]), int(last[r]) + 1
+            plans[r].run_local(dX, dY)
+            ref = smfv.SpmmPlan(smfv.Variant.SEQUENTIAL, plans[r].A, K, tiles="off")
+            Yr = torch.empty_like(dY)
+            ref.run(dX, Yr)
+            mabs, _ = smfv.compare(Yr[r0:r1], dY[r0:r1]) if r1 > r0 else (0.0, None)
+            ok = mabs == 0.0
+        print(json.dumps({"rank_only": sel[0], "p": p, "config": args.config, "variant": variant,
+                          "ranks": ranks, "partition": part,
+                          "check": {"ok": ok, "max_abs_diff": mabs,
+                                    "criterion": "ROWWISE: the rank's rows vs the 1-GPU untiled sequential plan "
+                                                 "(bit-identical); other variants: not assembled with one rank"}}))
+        if ok is False and not args.no_check:
+            sys.exit(3)
+        return
     if V != smfv.Variant.ROWWISE:
         xbuf = torch.full((max(int((off + cnt).max()), 1),), float("nan"), dtype=torch.float64, device=dev)
     for r in range(p):
@@ -1031,12 +1129,22 @@ def launch_ranks(n: int, argv: list[str]) -> int:
     return rc
 
 
-def dry_run(world: int, rank: int, local: int) -> None:
+def dry_run(args, world: int, rank: int, local: int) -> None:
     """--dry-run: the ranks start and meet (gloo), nothing touches the GPU;
-    rank 0 prints who came (tests the launcher on a CPU host)."""
+    rank 0 prints who came (tests the launcher on a CPU host) and (r6) the
+    CPU baseline the N-GPU line would carry, timed the same way (rank 0 first,
+    the others waiting in the rendezvous)."""
     import torch.distributed as dist
     me = {"rank": rank, "local_rank": local, "pid": os.getpid()}
     ranks = [me]
+    kind, K, variant = CONFIGS[args.config]
+    variant = args.variant or variant
+    cpu = None
+    if kind in ("cop20k", "cop20k_perm", "cop20k_irr"):
+        dl = Deadline(args.phase_timeout, rank, world, metric_for(args.config, K, variant))
+        cpu = rank0_cpu_baseline(args, world, rank, dl, lambda: cpu_baseline(
+            build_matrix(kind, args.mtx)[0], K, variant, sweep_ranks=False, ranks=cpu_ranks(world)))
+        dl.cancel()
     if world > 1:
         dist.init_process_group("gloo")
         ranks = [None] * world
@@ -1046,7 +1154,7 @@ def dry_run(world: int, rank: int, local: int) -> None:
     else:
         seen = 1
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": seen, "ranks": ranks}), flush=True)
+        print(json.dumps({"dry_run": True, "n_gpus": seen, "ranks": ranks, "cpu_baseline": cpu}), flush=True)
 
 
 def _devices_used(dev, world: int) -> int:
@@ -1124,6 +1232,9 @@ def main() -> None:
                     help="decomposed ROWWISE: also time the chunked exchange with this many row chunks per rank "
                          "(SMFV_DIST_CHUNKS; 1 = skip, the default: its point-to-point RCCL groups have not run on "
                          "more than one GPU yet, so the driver's run does not depend on them)")
+    ap.add_argument("--rank-only", type=int, default=-1,
+                    help="--rank-plans: time only this rank's plan (a PMC run of one rank's kernel); its share is "
+                         "checked against the 1-GPU sequential plan's rows")
     ap.add_argument("--rank-chunks", type=int, default=1,
                     help="--rank-plans ROWWISE: row chunks per rank plan (SMFV_DIST_CHUNKS; each chunk its own plan)")
     ap.add_argument("--xgmi-gbps", type=float, default=153.0,
@@ -1146,7 +1257,7 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.dry_run:
-        dry_run(world, rank, local)
+        dry_run(args, world, rank, local)
         return
     kind, K, variant = CONFIGS[args.config]
     variant = args.variant or variant
@@ -1169,15 +1280,19 @@ def main() -> None:
     cop = kind in ("cop20k", "cop20k_perm", "cop20k_irr")
 
     # CPU baseline first: rank 0 at N = 1, before anything touches the GPU
+    # (r6: at every N; rank 0, the other ranks wait in the gloo rendezvous)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        if cop:
-            cpu = cpu_baseline(A, K, variant)
+    if rank == 0 and not args.no_cpu_baseline:
+        if fallback is not None:
+            cpu = getattr(args, "cpu_baseline_done", None)  # timed by bench_decomposed before the GPU
+        elif cop:
+            cpu = cpu_baseline(A, K, variant, ranks=cpu_ranks(world))
         else:  # bounded stand-in: a 1M x 1M instance of the same generator (same row-length law)
             from sparsematrixmultiplicationmpi_amd import inputs
             S = inputs.gen_random_rows(1_000_000, 1_000_000, 16.0, 2.0, 4096, 42)
             cpu = cpu_baseline(S, K, variant, sample="bounded sample: 1M x 1M instance of the same power-law "
-                                                     f"generator (nnz {S.nnz}), K={K}", sweep_ranks=False)
+                                                     f"generator (nnz {S.nnz}), K={K}", sweep_ranks=False,
+                               ranks=cpu_ranks(world))
 
     import torch
     import torch.distributed as dist

@@ -302,6 +302,16 @@ SMFV_API int smfv_plan_destroy(smfv_plan_t plan);
  * non-temporal copy kernel.  Read + write bytes / time = the measured
  * streaming ceiling quoted beside the 8 TB/s spec. */
 SMFV_API int smfv_stream_copy(void *d_dst, const void *d_src, size_t bytes, void *stream);
+/* (r6) Floor probe of the SpMM's 2:1 read:write mix (bench only).
+ * unit_kib <= 0: a plain non-temporal stream, each 16 B written is the sum of
+ * 32 B read (rbytes == 2 * wbytes).  unit_kib in 1..64: the same kind of
+ * bytes through k_rows_ws's pipeline shape -- one 1024-lane block per CU,
+ * loader waves staging units of unit_kib KiB of d_src into LDS by
+ * non-temporal LDS-DMA (double-buffered), writer waves storing each unit's
+ * share of wbytes from LDS; rbytes < 2 GiB, rbytes >= wbytes.  d_dst gets
+ * no meaningful values. */
+SMFV_API int smfv_stream_mix(void *d_dst, size_t wbytes, const void *d_src, size_t rbytes, int unit_kib,
+                             void *stream);
 
 /* Rank-local building blocks of the distributed variants (also usable on
  * their own).  Row block [row_begin, row_end) of Y (row-major, ldy):
@@ -424,11 +434,14 @@ SMFV_API int smfv_dist_plan(int variant, int m, int64_t nnz, const int *h_row_pt
  *        is point to point: ncclSend of the chunk to every peer and ncclRecv
  *        of theirs (TO_ALL, an all-gatherv over the full xGMI mesh) or to the
  *        root (TO_ROOT, the Gatherv).  0 / 1: one block, one exchange.
+ *        EXPERIMENTAL: the schedule is pinned over gloo (2 / 3 / 8 ranks) and
+ *        at one rank on the GPU; its RCCL point-to-point groups have not yet
+ *        moved data between two GPUs, so bench.py defaults to --chunks 1.
  * Row-partitioned plans (A not replicated) always use the reference rows. */
 #define SMFV_DIST_BALANCED_ROWS (1 << 24)
 #define SMFV_DIST_CHUNKS(c) (((c) & 7) << 25)
 #define SMFV_DIST_CHUNKS_OF(f) (((f) >> 25) & 7)
-#define SMFV_DIST_OPTS (0xFF << 24)
+#define SMFV_DIST_OPTS ((int)0xFF000000u) /* (r6) no signed shift into the sign bit */
 /* smfv_dist_plan under distribution options (h_row_ptr needed for
  * work-balanced ROWWISE blocks; NULL falls back to the reference rows).
  * smfv_dist_plan(...) = smfv_dist_plan_opts(..., 0). */

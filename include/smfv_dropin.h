@@ -35,6 +35,10 @@
 // it come from the heap, not fresh mmaps) and M_TRIM_THRESHOLD = prefault +
 // 32 MiB (free heap up to that size stays mapped), for the rest of the
 // process.  Set SMFV_HEAP_PREFAULT_MB=0 to leave the allocator untouched.
+// (r6) The trim threshold is set first; if glibc then refuses the mmap
+// threshold, the trim threshold is put back to glibc's default (128 KiB), the
+// prefault is skipped and stderr says so.  Either successful mallopt turns
+// off glibc's dynamic thresholds for the process.
 // Returns its wall time (seconds).  Optional: the first call does
 // it otherwise, inside its own time.
 double smfvInitDevice();

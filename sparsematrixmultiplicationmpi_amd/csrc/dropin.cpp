@@ -875,8 +875,20 @@ static void prefault_heap()
     if (mb <= 0) return;
     const int mmap_thr = 32 << 20;
     const long trim_thr = std::min<long>((mb + 32) << 20, 0x7fffffffL);
-    if (mallopt(M_MMAP_THRESHOLD, mmap_thr) != 1 || mallopt(M_TRIM_THRESHOLD, (int)trim_thr) != 1) {
-        std::fprintf(stderr, "smfvInitDevice: mallopt refused the heap settings; heap prefault skipped\n");
+    // (r6) the trim threshold first: if the mmap threshold is then
+    // refused, the trim threshold goes back to glibc's default (128 KiB) and
+    // the message says what stays changed (glibc's dynamic thresholds are off
+    // after any successful mallopt of either)
+    if (mallopt(M_TRIM_THRESHOLD, (int)trim_thr) != 1) {
+        std::fprintf(stderr, "smfvInitDevice: mallopt refused M_TRIM_THRESHOLD; allocator untouched, heap prefault "
+                             "skipped\n");
+        return;
+    }
+    if (mallopt(M_MMAP_THRESHOLD, mmap_thr) != 1) {
+        const int restored = mallopt(M_TRIM_THRESHOLD, 128 * 1024);
+        std::fprintf(stderr, "smfvInitDevice: mallopt refused M_MMAP_THRESHOLD; M_TRIM_THRESHOLD %s glibc's default "
+                             "128 KiB (its dynamic mmap/trim thresholds stay off), heap prefault skipped\n",
+                     restored == 1 ? "restored to" : "could not be restored to");
         return;
     }
     const int nt = (int)std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency()));  // par_rows' threads

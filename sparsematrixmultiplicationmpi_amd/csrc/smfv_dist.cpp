@@ -858,23 +858,44 @@ SMFV_API int smfv_dist_plan_execute(smfv_dist_plan_t d, const int *d_row_ptr, co
         // plan's exchange stream and runs while chunk j + 1 computes; the
         // caller's stream waits for the last exchange.  (A capturing stream
         // forks to the exchange stream and joins back: graph-capturable.)
+        // EXPERIMENTAL: its point-to-point RCCL groups have been replayed over
+        // gloo and run at one rank, never between two GPUs.
         SMFV_REQUIRE(d_Y || d->m == 0 || d->K == 0, "null Y");
         hipStream_t st = smfv::as_stream(stream);
         const int K = d->K;
+        // (r6) once anything was forked to the exchange stream,
+        // every return joins it back: the caller's stream never runs ahead
+        // of an exchange that may still write d_Y
+        bool forked = false;
+        auto join = [&](int rc) -> int {
+            if (!forked) return rc;
+            hipError_t e1 = hipEventRecord(d->xdone, d->xst);
+            hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(st, d->xdone, 0) : e1;
+            if (e2 != hipSuccess) {
+                if (!rc) set_error("chunked execute join: %s", hipGetErrorString(e2));
+                // the join itself failed: drain the exchange stream so nothing is left writing d_Y
+                (void)hipStreamSynchronize(d->xst);
+                return rc ? rc : SMFV_ERR_HIP;
+            }
+            return rc;
+        };
         for (int j = 0; j < d->P.chunks; ++j) {
             if (d->cplans[(size_t)j]) {
                 int rc = smfv_plan_execute(d->cplans[(size_t)j], d_row_ptr, d_col_idx, d_values, d_X, K,
                                            d_Y + (int64_t)d->chunk_begin(j) * K, K, stream);
-                if (rc) return rc;
+                if (rc) return join(rc);
             }
-            SMFV_HIP_D(hipEventRecord(d->cev[(size_t)j], st));
-            SMFV_HIP_D(hipStreamWaitEvent(d->xst, d->cev[(size_t)j], 0));
+            hipError_t e = hipEventRecord(d->cev[(size_t)j], st);
+            if (e == hipSuccess) e = hipStreamWaitEvent(d->xst, d->cev[(size_t)j], 0);
+            if (e != hipSuccess) {
+                set_error("chunked execute fork (chunk %d): %s", j, hipGetErrorString(e));
+                return join(SMFV_ERR_HIP);
+            }
+            forked = true;
             int rc = run_exchange(d->comm, d->cops[(size_t)j], d_Y, d->xst);
-            if (rc) return rc;
+            if (rc) return join(rc);
         }
-        SMFV_HIP_D(hipEventRecord(d->xdone, d->xst));
-        SMFV_HIP_D(hipStreamWaitEvent(st, d->xdone, 0));
-        return SMFV_OK;
+        return join(SMFV_OK);
     }
     int rc = smfv_dist_plan_execute_local(d, d_row_ptr, d_col_idx, d_values, d_X, d_Y, stream);
     return rc ? rc : smfv_dist_plan_exchange(d, d_Y, stream);

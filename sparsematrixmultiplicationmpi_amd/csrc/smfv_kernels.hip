@@ -1332,6 +1332,74 @@ __global__ __launch_bounds__(256) void k_copy16(int64_t n16, const ws::d2 *__res
         if (base + 256 * k < n16) __builtin_nontemporal_store(a[k], dst + base + 256 * k);
 }
 
+// (r6) Floor probes of the SpMM's HBM mix (bench only; VERDICT r5 #2a).
+// The headline moves ~2 bytes read per byte written (CSR + X in, Y out),
+// which the 1:1 size-matched copy does not.  k_mix16: each lane reads two
+// 16-B pieces (non-temporal) and writes their sum -- the plain-load floor of
+// a 2:1 stream.  k_mix_lds: the same bytes through k_rows_ws's pipeline
+// shape -- one persistent 1024-lane block per CU, 8 loader waves stage unit
+// u + 1 (`ru` bytes) into one of two 64 KiB LDS slots by non-temporal
+// LDS-DMA while 8 writer waves store unit u's `wu` bytes from LDS
+// (non-temporal), one barrier per unit: the floor of the staged design at a
+// given unit size.
+__global__ __launch_bounds__(256) void k_mix16(int64_t w16, const ws::d2 *__restrict__ src,
+                                               ws::d2 *__restrict__ dst)
+{
+    const int64_t base = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+    ws::d2 a[4], b[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (base + 256 * k < w16) {
+            a[k] = __builtin_nontemporal_load(src + 2 * (base + 256 * k));
+            b[k] = __builtin_nontemporal_load(src + 2 * (base + 256 * k) + 1);
+        }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        if (base + 256 * k < w16) __builtin_nontemporal_store(a[k] + b[k], dst + base + 256 * k);
+}
+
+__global__ __launch_bounds__(1024, 1) void k_mix_lds(int64_t rbytes, int64_t wbytes, int nunits, int ru, int wu,
+                                                     const char *__restrict__ src, char *__restrict__ dst)
+{
+    using namespace ws;
+    constexpr int SLOT = 65536;
+    __shared__ __attribute__((aligned(16))) char lds[2 * SLOT];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nb = gridDim.x;
+    const int cnt = (int)blockIdx.x < nunits ? (nunits - 1 - (int)blockIdx.x) / nb + 1 : 0;
+    if (cnt == 0) return;  // block-uniform
+    const unsigned lds0 = (unsigned)(uintptr_t)lds;
+    if (wv >= 8) {
+        __builtin_amdgcn_s_setprio(3);
+        const int wl = wv - 8;
+        auto stage = [&](int u, int slot) {
+            const int64_t base = (int64_t)u * ru;
+            const char *sb = src + base;
+            for (int k = wl; k * 1024 < ru; k += 8)
+                if (base + k * 1024 + 16 * lane < rbytes) dma16s<true>(sb, 1024u * k + 16u * lane, lds0 + slot * SLOT + k * 1024);
+        };
+        stage((int)blockIdx.x, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        barrier_lds();
+        for (int i = 0; i < cnt; ++i) {
+            if (i + 1 < cnt) stage((int)blockIdx.x + (i + 1) * nb, (i + 1) & 1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            barrier_lds();
+        }
+        return;
+    }
+    barrier_lds();
+    for (int i = 0; i < cnt; ++i) {
+        const int u = (int)blockIdx.x + i * nb;
+        const char *sl = lds + (i & 1) * SLOT;
+        const int64_t wb = (int64_t)u * wu;
+        for (int k = tid; k * 16 < wu; k += 512)
+            if (wb + 16 * k < wbytes)
+                __builtin_nontemporal_store(*reinterpret_cast<const d2 *>(sl + (16 * k) % ru),
+                                            reinterpret_cast<d2 *>(dst + wb + 16 * k));
+        barrier_lds();
+    }
+}
+
 // smfv_device_init: loads the code object, computes nothing
 __global__ void k_noop() {}
 
@@ -2777,6 +2845,41 @@ SMFV_API int smfv_stream_copy(void *d_dst, const void *d_src, size_t bytes, void
     return SMFV_OK;
 }
 
+SMFV_API int smfv_stream_mix(void *d_dst, size_t wbytes, const void *d_src, size_t rbytes, int unit_kib,
+                             void *stream)
+{
+    SMFV_REQUIRE(d_dst && d_src && aligned16(d_dst) && aligned16(d_src) && wbytes % 16 == 0 && rbytes % 16 == 0,
+                 "mix probe needs 16-byte aligned pointers and sizes");
+    if (wbytes == 0) return SMFV_OK;
+    hipStream_t st = as_stream(stream);
+    if (unit_kib <= 0) {
+        SMFV_REQUIRE(rbytes == 2 * wbytes, "plain mix probe reads exactly twice the bytes it writes");
+        const int64_t w16 = (int64_t)(wbytes / 16), nblk = (w16 + 1023) / 1024;
+        SMFV_REQUIRE(nblk <= 0x7fffffff, "mix too large");
+        hipLaunchKernelGGL(k_mix16, dim3((unsigned)nblk), dim3(256), 0, st, w16, static_cast<const ws::d2 *>(d_src),
+                           static_cast<ws::d2 *>(d_dst));
+        SMFV_LAUNCHED();
+        return SMFV_OK;
+    }
+    SMFV_REQUIRE(unit_kib <= 64 && rbytes >= wbytes, "LDS mix probe: units of at most 64 KiB, reads >= writes");
+    SMFV_REQUIRE(rbytes < (1ull << 31), "LDS mix probe: under 2 GiB read");
+    const int ru = unit_kib * 1024;
+    const int64_t nunits = ((int64_t)rbytes + ru - 1) / ru;
+    // the unit's write share, rounded up to 16 B so the units cover wbytes
+    const int wu = (int)((((int64_t)wbytes + nunits - 1) / nunits + 15) / 16 * 16);
+    SMFV_REQUIRE(wu <= ru, "LDS mix probe: a unit writes more than it stages");
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ncu = v;
+    }
+    const int blocks = (int)std::min<int64_t>(nunits, ncu);
+    hipLaunchKernelGGL(k_mix_lds, dim3((unsigned)blocks), dim3(1024), 0, st, (int64_t)rbytes, (int64_t)wbytes,
+                       (int)nunits, ru, wu, static_cast<const char *>(d_src), static_cast<char *>(d_dst));
+    SMFV_LAUNCHED();
+    return SMFV_OK;
+}
+
 SMFV_API int smfv_plan_destroy(smfv_plan_t plan)
 {
     delete plan;
@@ -2924,9 +3027,12 @@ SMFV_API int smfv_plan_execute(smfv_plan_t plan, const int *d_row_ptr, const int
             chunked = (chunked & 1) | (K << 16);
         }
         if (plan->live) {
-            if (!saddr) {
-                set_error("live-values tiled plan: X must span < 4 GiB (n * ldx * 8)");
-                return SMFV_ERR_INVALID;
+            if (!saddr || (uint64_t)plan->nnz * 8u >= (1ull << 32)) {
+                // (r6) X (or the block's values) spanning 4 GiB or
+                // more: the untiled row kernel on the same live values, as the
+                // wsn branch does (bit-identical: each row in CSR order)
+                return launch_rows(plan->row_begin, m, d_row_ptr, d_col_idx, d_values, d_X, ldx, plan->n, K, d_Y,
+                                   ldy, st);
             }
             // the value pairs come from the block's CSR values through a
             // range-checked buffer (the last odd row's read past the end gives 0)

@@ -85,6 +85,15 @@ def test_gpus_n_starts_n_ranks_itself():
     assert sorted(x["rank"] for x in line["ranks"]) == [0, 1]
     assert len({x["pid"] for x in line["ranks"]}) == 2 and os.getpid() not in {x["pid"] for x in line["ranks"]}
     assert line["launcher"]["ranks_started"] == 2
+    # (r6) the N = 2 line carries the CPU/MPI baseline: the
+    # reference's kernel under mpiexec, 16 ranks per GPU capped at the CPUs
+    # available, timed by rank 0 before any GPU call
+    cpu = line["cpu_baseline"]
+    assert cpu is not None and cpu["value"] > 0 and cpu["unit"] == "GFLOP/s"
+    if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "ref_driver")):
+        assert cpu["kind"] == "reference"
+        assert cpu["cores"] == min(32, len(os.sched_getaffinity(0)))
+        assert "2-GPU line" in cpu["note_n_gpus"]
 
 
 def test_gpus_must_match_world_size():

@@ -103,9 +103,9 @@ def check(variant, g, p, Y):
 def test_rank_plans_vs_reference(gpu, name, p, variant, partition, tiles):
     """Every rank's plan (smfv_dist_plan_create_rank) + the native exchange
     schedule replayed on the device = the reference's result at p ranks.
-    (r5) ROWWISE under both row partitions: the reference's equal rows and
-    the plans' default equal-work blocks (same bytes: a row is summed by one
-    rank in CSR order either way)."""
+    (r5) ROWWISE under both row partitions: the reference's equal rows (the
+    default) and the opt-in equal-work blocks, SMFV_DIST_BALANCED_ROWS (same
+    bytes: a row is summed by one rank in CSR order either way)."""
     g, A, dA, dX = golden_problem(name, gpu)
     K = dX.shape[1]
     root = p - 1  # a root other than 0 where p > 1

@@ -40,9 +40,11 @@ def standin(request, gpu):
     return request.param, A, X, Yseq, absY, smfv.DeviceCSR(A, gpu), torch.from_numpy(X).to(gpu)
 
 
-# (r5) ROWWISE under the three row partitions: blocks of equal work (the
-# default), the reference's equal rows, and equal-work blocks cut into 3
-# chunks (SMFV_DIST_CHUNKS: one tiled plan per chunk)
+# (r5) ROWWISE under the row partitions: blocks of equal work (opt-in,
+# SMFV_DIST_BALANCED_ROWS), the reference's equal rows (the default,
+# SC/...RowWise.cpp:26-29), and equal-work blocks cut into 3 chunks
+# (SMFV_DIST_CHUNKS: one tiled plan per chunk).  COLUMNWISE / NONZERO ignore
+# the row partition (their own reference decompositions)
 PARTS = [(smfv.Variant.ROWWISE, "balanced", 1), (smfv.Variant.ROWWISE, "reference", 1),
          (smfv.Variant.ROWWISE, "balanced", 3), (smfv.Variant.COLUMNWISE, "balanced", 1),
          (smfv.Variant.NONZERO, "balanced", 1)]
