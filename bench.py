@@ -104,6 +104,18 @@ def measured_traffic(config: str, kernel: str):
     return e["traffic_bytes_per_launch"], e["source"]
 
 
+def lds_staged_bytes(st: dict, K: int):
+    """(r6) Bytes a k_rows_ws plan moves into LDS per launch: every tile's X
+    union once per 32-column panel (staged_rows * 8 K), plus its meta once
+    (values snapshot 8 B + u8 offset 1 B per entry, 1 KiB record per tile).
+    Mostly L2 / MALL hits: the HBM side is roofline.traffic."""
+    if st.get("kernel") != "k_rows_ws" or not st.get("tiled"):
+        return None
+    x = st["staged_rows"] * 8 * K
+    meta = st["snapshot_entries"] * 9 + st["tiles"] * 1024
+    return {"x_images": int(x), "meta": int(meta), "total": int(x + meta)}
+
+
 def measured_rank_traffic(config: str, p: int, rank: int, kernel: str):
     """(r6) Per-launch HBM bytes of rank `rank`'s plan of the p-rank
     decomposition (profiles/pmc_traffic.json key '<config>@p<p>r<rank>',
@@ -332,6 +344,51 @@ def size_matched_copy(dev, prob_bytes: int, ncopies: int, steps: int, world: int
             "GBps": round(2 * half / (ms * 1e-3) / 1e9, 1),
             "note": "smfv_stream_copy of the algorithmic bytes per launch, cold rotation, one graph of the "
                     "timed step count; frac_of_copy_time = copy time / SpMM time"}
+
+
+def mix_matched_copy(dev, rbytes: int, wbytes: int, ncopies: int, steps: int, world: int) -> dict | None:
+    """(r6, VERDICT r5 #2a) The floor of the SpMM's own byte MIX: it reads ~2
+    bytes (CSR + X) per byte written (Y), where size_matched_copy is 1:1.
+    smfv_stream_mix moves the SpMM's algorithmic read and write bytes per
+    launch under the same rotation and timing, three ways: `plain` (each lane
+    reads 32 B non-temporally and writes their 16-B sum), and `lds32` /
+    `lds64` (k_rows_ws's pipeline shape: 1024-lane block per CU, loader waves
+    LDS-DMA units of 32 / 64 KiB into two LDS slots, writer waves store from
+    LDS, one barrier per unit; lds32 runs ~7.5 units per CU, the headline
+    plan's 7.9).  None where the rotation would not fit (> 8 GiB)."""
+    import torch
+    from sparsematrixmultiplicationmpi_amd._lib import call
+    w = (wbytes // 16) * 16
+    r = 2 * w  # the plain probe reads exactly 2x; the LDS probes take the real read bytes below
+    rr = (rbytes // 16) * 16
+    if w <= 0 or ncopies * (max(r, rr) + w) > (8 << 30):
+        return None
+    bufs = [(torch.empty(max(r, rr) // 8, dtype=torch.float64, device=dev),
+             torch.empty(w // 8, dtype=torch.float64, device=dev)) for _ in range(ncopies)]
+    for a, _ in bufs:
+        a.fill_(1.0)
+    out = {"read_bytes_per_launch": rr, "write_bytes_per_launch": w,
+           "note": "smfv_stream_mix, cold rotation over the SpMM's copy count, one graph of the timed step count; "
+                   "plain reads 2x the write bytes (32 B per 16 B written); frac_of_spmm_time = probe / SpMM time"}
+    for name, unit, nread in (("plain", 0, r), ("lds32", 32, rr), ("lds64", 64, rr)):
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g, stream=side):
+                st = torch.cuda.current_stream().cuda_stream
+                for i in range(steps):
+                    a, b = bufs[i % ncopies]
+                    call("smfv_stream_mix", b.data_ptr(), w, a.data_ptr(), nread, unit, st)
+        torch.cuda.current_stream().wait_stream(side)
+        _stabilize(g)
+        ms = _timed_events(g.replay, world) / steps
+        del g
+        out[name] = {"avg_launch_ms": round(ms, 6), "bytes_per_launch": nread + w,
+                     "GBps": round((nread + w) / (ms * 1e-3) / 1e9, 1)}
+    del bufs
+    torch.cuda.empty_cache()
+    return out
 
 
 def _stabilize(g) -> int:
@@ -1437,6 +1494,9 @@ def main() -> None:
     span_ms_w = timed(capture(True)) if not args.no_warm else float("nan")
     stream_gbps = stream_copy_gbps(dev)
     copy_floor = size_matched_copy(dev, prob_bytes, ncopies, args.steps, world) if not args.no_copy_floor else None
+    wr_bytes = 8 * m * K
+    mix_floor = (mix_matched_copy(dev, prob_bytes - wr_bytes, wr_bytes, ncopies, args.steps, world)
+                 if not args.no_copy_floor else None)
     vendor = None
     if variant in ("ROWWISE", "SEQUENTIAL") and not args.no_vendor:
         vendor = vendor_leg(copies, args, timed, 2.0 * nnz * K)
@@ -1511,7 +1571,11 @@ def main() -> None:
                          "stream_copy_GBps": round(stream_gbps, 1),
                          "frac_of_stream_copy": round(achieved / stream_gbps, 4) if stream_gbps else None,
                          "size_matched_copy": (dict(copy_floor, frac_of_copy_time=round(copy_floor["avg_launch_ms"] / kern_ms, 4))
-                                               if copy_floor else None)},
+                                               if copy_floor else None),
+                         "mix_matched_copy": (dict(mix_floor, **{f"frac_of_spmm_time_{k}": round(
+                             mix_floor[k]["avg_launch_ms"] / kern_ms, 4) for k in ("plain", "lds32", "lds64")})
+                                              if mix_floor else None),
+                         "lds_staged_bytes_per_launch": lds_staged_bytes(st, K)},
             "plan": {"tiled": st["tiled"], "tiles": st["tiles"], "reuse": round(st["reuse"], 3),
                      "live_values": st["live_values"], "paired_rows": st.get("paired_rows"),
                      "est_reuse_sampled": round(st["est_reuse"], 3), "direct_rows": st["direct_rows"],

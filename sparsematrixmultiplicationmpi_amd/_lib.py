@@ -122,6 +122,7 @@ _SIGS = {
     "smfv_dist_plan_stats": (c_int, [c_void_p, _PD]),
     "smfv_dist_plan_destroy": (c_int, [c_void_p]),
     "smfv_stream_copy": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "smfv_stream_mix": (c_int, [c_void_p, c_size_t, c_void_p, c_size_t, c_int, c_void_p]),
     "smfv_vendor_spmm_create": (c_int, [c_void_p, c_int, c_int, c_int, c_int64, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_int64, c_int, c_void_p, c_int64, c_void_p]),
     "smfv_vendor_spmm_execute": (c_int, [c_void_p]),
