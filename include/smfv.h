@@ -257,10 +257,14 @@ SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_
 /* (r5) The narrow-team plan of a kw = 4 / 8 column window (k_rows_wsn) for
  * the row block [row_begin, row_end), built and verified on the host (the
  * kernel's reads replayed): out[0] tiles, [1] staged X rows, [2] re-use,
- * [3] direct rows, [4] rows of the fullest tile, [5] padded entries.  No
+ * [3] direct rows, [4] rows of the fullest tile, [5] padded entries; (r6)
+ * the modelled LDS cycles of the kernel's X reads (ds_read_b128 lane groups,
+ * one cycle each when conflict-free, plus one per extra distinct address on a
+ * bank): [6] lane groups (the conflict-free count), [7] cycles with the
+ * plan's bank-coloured image slots, [8] cycles with first-use slots.  No
  * device needed.  (SC/...ColumnWise.cpp:34-48 on a rank's K/p panel.) */
 SMFV_API int smfv_wsn_plan_analyse(int row_begin, int row_end, int n, const int *h_row_ptr,
-                                   const int *h_col_idx, int kw, double out[6]);
+                                   const int *h_col_idx, int kw, double out[9]);
 SMFV_API int smfv_plan_analyse_rows(int row_begin, int row_end, int n, const int *h_row_ptr,
                                     const int *h_col_idx, int flags, double out[9]);
 /* The K = 1 chunk layout (k_spmv_chunks) of the row block [row_begin,

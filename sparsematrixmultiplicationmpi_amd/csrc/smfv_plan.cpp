@@ -1245,6 +1245,155 @@ bool verify_wsn_plan(int m, int n, const int *rp, const int *ci, const WsnPlan &
 }  // namespace
 
 namespace {
+// (r6) Image slots of a tile's union rows, coloured for the
+// LDS banks of k_rows_wsn's X reads.  A team reads its entry's image row
+// (XROW = 32 / 64 B: 8 / 16 of the 64 banks) with one ds_read_b128, whose 64
+// lanes are serviced in 4 lane groups of 16 ({0-3,12-15,20-27},
+// {4-11,16-19,28-31}, the same + 32): 8 teams of 2 lanes (KW = 4) or 4 of 4
+// (KW = 8) per group.  Image row s sits in bank group s mod C (C = 256 /
+// XROW = 8 / 4), so two teams of one lane group that read different rows of
+// one colour in the same instruction conflict (each extra distinct address
+// on a bank costs an LDS cycle: a group's cycles = its most-loaded colour).
+// The plan is free to put any union row in any image slot, so this colours
+// the union rows: the lane groups of every (wave, batch, entry) instruction
+// are collected (teams still running in that batch; pads read the zero row,
+// colour ucap mod C, all at one address), then each union row -- most-read
+// first -- takes the colour that meets the fewest rows already placed in its
+// groups, with at most ceil(nu / C) + 1 rows per colour; two refinement
+// passes move single rows.  Colour c's i-th row gets slot c + C i; the image
+// then has S >= nu rows (holes stage X row 0, unread).  `cycles` models the
+// LDS cycles of the tile's X reads (one per non-empty lane group, plus its
+// conflicts); `plain` the same for first-use slots (slot = union position).
+struct WsnSlots {
+    std::vector<int> slot;  // union position -> image row
+    int S = 0;              // image rows staged
+    int64_t groups = 0, cycles = 0, plain = 0;
+};
+
+inline int b128_lane_group(int l)
+{
+    const int h = l & 31;
+    const bool a = h < 4 || (h >= 12 && h < 16) || (h >= 20 && h < 28);
+    return (l >> 5) * 2 + (a ? 0 : 1);
+}
+
+WsnSlots colour_wsn_slots(const WsnGeom &G, const int *rp, const int *ci, const std::vector<int> &Rw,
+                          const std::vector<int> &pos, int nu, bool colour)
+{
+    WsnSlots W;
+    const int TW = G.tw(), TL = G.tl(), C = 256 / G.xrow(), ZC = G.ucap % C;
+    const int PAD = nu;  // the zero row, as a member id
+    auto nbat = [&](int r) { return std::max(1, (rp[r + 1] - rp[r] + WSN_B - 1) / WSN_B); };
+    // (group key, member) for every running team's entry
+    std::vector<std::pair<int64_t, int>> mem;
+    const int maxb = Rw.empty() ? 1 : nbat(Rw[0]) + 1;
+    for (int q = 0; q < 8 && (size_t)q * TW < Rw.size(); ++q) {
+        const int nt_q = (int)std::min<size_t>(TW, Rw.size() - (size_t)q * TW);
+        for (int k = 0; k < nt_q; ++k) {
+            const int r = Rw[(size_t)(q * TW + k)], rl = rp[r + 1] - rp[r], lg = b128_lane_group(k * TL);
+            for (int b = 0; b < nbat(r); ++b)
+                for (int e = 0; e < WSN_B; ++e) {
+                    const int el = WSN_B * b + e;
+                    const int64_t key = (((int64_t)q * maxb + b) * WSN_B + e) * 4 + lg;
+                    mem.emplace_back(key, el < rl ? pos[ci[rp[r] + el]] : PAD);
+                }
+        }
+    }
+    std::sort(mem.begin(), mem.end());
+    mem.erase(std::unique(mem.begin(), mem.end()), mem.end());  // one address reads once (broadcast)
+    // groups as ranges of mem; per union row, the groups it is read in
+    std::vector<int> gstart;
+    for (size_t i = 0; i < mem.size(); ++i)
+        if (i == 0 || mem[i].first != mem[i - 1].first) gstart.push_back((int)i);
+    const int ng = (int)gstart.size();
+    gstart.push_back((int)mem.size());
+    W.groups = ng;
+    std::vector<int> deg((size_t)nu + 1, 0), gof((size_t)mem.size());
+    for (int g = 0; g < ng; ++g)
+        for (int i = gstart[g]; i < gstart[g + 1]; ++i) {
+            gof[(size_t)i] = g;
+            ++deg[(size_t)mem[(size_t)i].second];
+        }
+    std::vector<int> cptr((size_t)nu + 2, 0), cg((size_t)mem.size());
+    for (int u = 0; u <= nu; ++u) cptr[(size_t)u + 1] = cptr[(size_t)u] + deg[(size_t)u];
+    {
+        std::vector<int> fill(cptr.begin(), cptr.end() - 1);
+        for (size_t i = 0; i < mem.size(); ++i) cg[(size_t)fill[(size_t)mem[i].second]++] = gof[i];
+    }
+    auto model = [&](const std::vector<int> &col) {  // LDS cycles: per group its most-loaded colour
+        int64_t cyc = 0;
+        std::vector<int> cnt((size_t)C);
+        for (int g = 0; g < ng; ++g) {
+            std::fill(cnt.begin(), cnt.end(), 0);
+            int mx = 0;
+            for (int i = gstart[g]; i < gstart[g + 1]; ++i) {
+                const int u = mem[(size_t)i].second;
+                mx = std::max(mx, ++cnt[(size_t)(u == PAD ? ZC : col[(size_t)u])]);
+            }
+            cyc += mx;
+        }
+        return cyc;
+    };
+    std::vector<int> plain((size_t)nu);
+    for (int u = 0; u < nu; ++u) plain[(size_t)u] = u % C;
+    W.plain = model(plain);
+    auto first_use = [&]() {
+        W.slot.resize((size_t)nu);
+        for (int u = 0; u < nu; ++u) W.slot[(size_t)u] = u;
+        W.S = nu;
+        W.cycles = W.plain;
+        return W;
+    };
+    if (!colour || nu == 0) return first_use();
+    // capacity per colour: slots c + C i below the zero row (ucap)
+    const int want = (nu + C - 1) / C + 1;
+    std::vector<int> cap((size_t)C), used((size_t)C, 0);
+    for (int c = 0; c < C; ++c) cap[(size_t)c] = std::min(want, (G.ucap - c + C - 1) / C);
+    std::vector<int> cnt((size_t)ng * C, 0), col((size_t)nu, -1);
+    for (int g = 0; g < ng; ++g)
+        if (mem[(size_t)gstart[g]].second == PAD || mem[(size_t)gstart[g + 1] - 1].second == PAD)
+            cnt[(size_t)g * C + ZC] = 1;  // (PAD sorts last in its group)
+    std::vector<int> order((size_t)nu);
+    for (int u = 0; u < nu; ++u) order[(size_t)u] = u;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return deg[(size_t)a] > deg[(size_t)b]; });
+    auto place = [&](int u) {
+        int best = -1;
+        int64_t bc = 0;
+        for (int c = 0; c < C; ++c) {
+            if (used[(size_t)c] >= cap[(size_t)c]) continue;
+            int64_t cost = 0;
+            for (int i = cptr[(size_t)u]; i < cptr[(size_t)u + 1]; ++i) cost += cnt[(size_t)cg[(size_t)i] * C + c];
+            if (best < 0 || cost < bc || (cost == bc && used[(size_t)c] < used[(size_t)best])) best = c, bc = cost;
+        }
+        if (best < 0) return false;
+        col[(size_t)u] = best;
+        ++used[(size_t)best];
+        for (int i = cptr[(size_t)u]; i < cptr[(size_t)u + 1]; ++i) ++cnt[(size_t)cg[(size_t)i] * C + best];
+        return true;
+    };
+    for (int u : order)
+        if (!place(u)) return first_use();
+    for (int pass = 0; pass < 2; ++pass)
+        for (int u : order) {
+            const int c0 = col[(size_t)u];
+            --used[(size_t)c0];
+            for (int i = cptr[(size_t)u]; i < cptr[(size_t)u + 1]; ++i) --cnt[(size_t)cg[(size_t)i] * C + c0];
+            place(u);  // (its own colour has room again: always placed)
+        }
+    const int64_t cyc = model(col);
+    if (cyc >= W.plain) return first_use();  // never worse than first-use slots
+    W.cycles = cyc;
+    W.slot.assign((size_t)nu, 0);
+    std::vector<int> next((size_t)C, 0);
+    W.S = 0;
+    for (int u = 0; u < nu; ++u) {
+        const int c = col[(size_t)u];
+        W.slot[(size_t)u] = c + C * next[(size_t)c]++;
+        W.S = std::max(W.S, W.slot[(size_t)u] + 1);
+    }
+    return W;
+}
+
 bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPlan &P, std::string *err,
                        const TileCaps &caps_in, int frac_num, int frac_den)
 {
@@ -1345,7 +1494,13 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
         const int nu = (int)ucols.size();
         int *g = &P.grec[(size_t)t * WSN_GWORDS];
         int *l = &P.lrec[(size_t)t * LWD];
-        for (int u = 0; u < nu; ++u) g[u] = ucols[(size_t)u];
+        // (r6) union rows in bank-coloured image slots (holes: X row 0, unread)
+        const WsnSlots SL = colour_wsn_slots(G, rp, ci, Rw, pos, nu, caps.wsn_colour);
+        for (int u = 0; u < nu; ++u) g[SL.slot[(size_t)u]] = ucols[(size_t)u];
+        P.x_groups += SL.groups;
+        P.x_cycles += SL.cycles;
+        P.x_cycles_plain += SL.plain;
+        P.staged_rows += SL.S;
         for (int s = 0; s < R; ++s) l[s] = -1;
         // wave group q (TW consecutive rows of the sorted list) -> wave w;
         // groups q and 7 - q share a SIMD (waves w and w + 4)
@@ -1374,7 +1529,7 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
                 for (int j = rp[r]; j < rp[r + 1]; ++j) {
                     const int el = j - rp[r], b = el / WSN_B, e = el % WSN_B;
                     P.loff[(size_t)(noff + WSN_B * (int64_t)(lbase[w] + cum[(size_t)b] + k) + e)] =
-                        (uint16_t)pos[ci[j]];
+                        (uint16_t)SL.slot[(size_t)pos[ci[j]]];
                     P.tsrc[(size_t)(noff +
                                     2 * (int64_t)(vbase[w] + 2 * cum[(size_t)b] + (e / 2) * nb_at[(size_t)b] + k) +
                                     e % 2)] = j;
@@ -1389,7 +1544,7 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
         for (int q = 0; q < 16; ++q) {
             g[WSN_G_NOFF + q] = (int)noff;
             g[WSN_G_TN + q] = (int)(toff[(size_t)t + 1] - noff);
-            g[WSN_G_NU + q] = nu;
+            g[WSN_G_NU + q] = SL.S;
             g[WSN_G_VOFF + q] = (int)noff;
             g[WSN_G_TNV + q] = (int)(toff[(size_t)t + 1] - noff);
         }
@@ -1420,10 +1575,12 @@ bool build_wsn_plan(int m, int n, const int *rp, const int *ci, int kw, WsnPlan 
         return r;
     };
     bool any = false;
+    TileCaps cs = caps;
+    if (std::getenv("SMFV_WSN_FIRST_USE_SLOTS")) cs.wsn_colour = false;  // (r6) A/B of the slot colouring
     for (const auto &f : fr) {
         WsnPlan Q;
         std::string e;
-        if (!build_wsn_plan_at(m, n, rp, ci, kw, Q, &e, caps, f[0], f[1])) {
+        if (!build_wsn_plan_at(m, n, rp, ci, kw, Q, &e, cs, f[0], f[1])) {
             if (err && !any) *err = e;
             continue;
         }

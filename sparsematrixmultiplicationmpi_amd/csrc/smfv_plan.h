@@ -143,6 +143,9 @@ struct TileCaps {
     int team_rows = 0;
     int pair_len = 56;
     int pair_slack = 1;            // batches a pair may run past the longest row
+    // (r6) build_wsn_plan: union rows in bank-coloured image slots
+    // (colour_wsn_slots, smfv_plan.cpp); false: first-use order
+    bool wsn_colour = true;
 };
 // Independent parts are analysed on up to 8 threads; analysis_threads > 0
 // caps that for analyses run on the calling thread (smfv_set_analysis_threads).
@@ -257,6 +260,10 @@ struct WsnPlan {
     std::vector<int> direct;       // rows over a cap alone
     int64_t union_rows = 0, tiled_nnz = 0, entries = 0, ventries = 0;
     int xcd[9] = {};
+    // (r6) image rows staged (union rows + the colouring's holes), and the
+    // modelled LDS cycles of the X reads: lane groups (= cycles without any
+    // bank conflict), with the plan's slots, with first-use slots
+    int64_t staged_rows = 0, x_groups = 0, x_cycles = 0, x_cycles_plain = 0;
 };
 // Tiles from analyse_tiles (caps.ucap / ncap / maxrows follow the geometry;
 // caps.part_* as for build_ws_plan), each laid out per wave; a tile whose

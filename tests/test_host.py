@@ -678,10 +678,10 @@ def test_narrow_team_plan_on_host():
     ip = ctypes.POINTER(ctypes.c_int)
 
     def wsn(A, kw, r0=0, r1=None):
-        out = (ctypes.c_double * 6)()
+        out = (ctypes.c_double * 9)()
         _lib.call("smfv_wsn_plan_analyse", r0, A.numRows if r1 is None else r1, A.numCols,
                   A.rowPtr.ctypes.data_as(ip), A.colIndices.ctypes.data_as(ip), kw, out)
-        return [float(v) for v in out]
+        return [float(v) for v in out[:6]]
     A = smfv.inputs.cop20k_surrogate()
     for kw, rows in ((4, 256), (8, 128)):
         tiles, union, reuse, direct, most, entries = wsn(A, kw)
