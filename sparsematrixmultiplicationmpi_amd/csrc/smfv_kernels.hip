@@ -2658,7 +2658,7 @@ SMFV_API int smfv_plan_analyse(int m, int n, const int *h_row_ptr, const int *h_
 }
 
 SMFV_API int smfv_wsn_plan_analyse(int row_begin, int row_end, int n, const int *h_row_ptr_all,
-                                   const int *h_col_idx_all, int kw, double out[6])
+                                   const int *h_col_idx_all, int kw, double out[9])
 {
     SMFV_REQUIRE(row_begin >= 0 && row_end >= row_begin && n >= 0 && h_row_ptr_all && h_col_idx_all && out &&
                      (kw == 4 || kw == 8),
@@ -2688,6 +2688,9 @@ SMFV_API int smfv_wsn_plan_analyse(int row_begin, int row_end, int n, const int 
     out[3] = (double)W.direct.size();
     out[4] = (double)most;
     out[5] = (double)W.entries;
+    out[6] = (double)W.x_groups;
+    out[7] = (double)W.x_cycles;
+    out[8] = (double)W.x_cycles_plain;
     return SMFV_OK;
 }
 
