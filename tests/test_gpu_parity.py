@@ -286,6 +286,40 @@ def test_compare_and_fill(gpu):
     assert torch.equal(X, X2)
 
 
+def test_mix_floor_probe_moves_the_bytes(gpu):
+    """(r6) The 2:1 floor probes bench.py reports (roofline.mix_matched_copy)
+    really move their bytes: plain mode writes the sum of each 32-B pair it
+    reads; the LDS-DMA mode writes, for unit u of ru bytes, the bytes its
+    loaders staged (dst[u wu + i] = src[u ru + i mod ru] wherever that
+    source byte exists).  Sizes like the headline's ratio, small."""
+    from sparsematrixmultiplicationmpi_amd._lib import call
+    st = torch.cuda.current_stream().cuda_stream
+    w = 3 * 1000 * 1024 + 48  # not a multiple of the unit: ragged last unit
+    src = torch.randn(2 * w // 8, dtype=torch.float64, device=gpu)
+    dst = torch.zeros(w // 8, dtype=torch.float64, device=gpu)
+    call("smfv_stream_mix", dst.data_ptr(), w, src.data_ptr(), 2 * w, 0, st)
+    torch.cuda.synchronize()
+    pairs = src.view(-1, 2, 2)  # 16-B pieces of two doubles
+    assert torch.equal(dst.view(-1, 2), pairs[:, 0, :] + pairs[:, 1, :])
+    for unit_kib in (32, 64):
+        r = 2 * w - 16 * 37  # reads >= writes, ragged
+        dst.zero_()
+        call("smfv_stream_mix", dst.data_ptr(), w, src.data_ptr(), r, unit_kib, st)
+        torch.cuda.synchronize()
+        ru = unit_kib * 1024
+        nunits = (r + ru - 1) // ru
+        wu = ((w + nunits - 1) // nunits + 15) // 16 * 16
+        sb = src.view(torch.uint8).cpu().numpy()
+        db = dst.view(torch.uint8).cpu().numpy()
+        for u in range(nunits):
+            i = np.arange(u * wu, min((u + 1) * wu, w))
+            srci = u * ru + (i - u * wu) % ru
+            ok = srci < r
+            assert np.array_equal(db[i[ok]], sb[srci[ok]]), (unit_kib, u)
+    with pytest.raises(RuntimeError):  # plain mode reads exactly twice what it writes
+        call("smfv_stream_mix", dst.data_ptr(), w, src.data_ptr(), w, 0, st)
+
+
 def test_reference_api_functions(gpu):
     """The reference's four entry points (host arrays in/out), single process."""
     g = load_golden("fem1k_k32")
