@@ -2668,6 +2668,7 @@ SMFV_API int smfv_wsn_plan_analyse(int row_begin, int row_end, int n, const int 
     for (int i = 0; i <= m; ++i) rpl[i] = h_row_ptr_all[row_begin + i] - h_row_ptr_all[row_begin];
     const int *cil = h_col_idx_all + h_row_ptr_all[row_begin];
     TileCaps caps = plan_caps(0, row_begin);
+    caps.wsn_model = true;  // (r6) report the X reads' modelled LDS cycles
     double footprint = -1.0;
     plan_parts(caps, 0, m, n, rpl.data(), cil, &footprint);
     WsnPlan W;

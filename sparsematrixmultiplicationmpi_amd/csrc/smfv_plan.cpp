@@ -1278,15 +1278,25 @@ inline int b128_lane_group(int l)
 }
 
 WsnSlots colour_wsn_slots(const WsnGeom &G, const int *rp, const int *ci, const std::vector<int> &Rw,
-                          const std::vector<int> &pos, int nu, bool colour)
+                          const std::vector<int> &pos, int nu, bool colour, bool model_only_if_colour = true)
 {
     WsnSlots W;
+    if (!colour && model_only_if_colour) {  // first-use slots, no model (the fast path of the fraction search)
+        W.slot.resize((size_t)nu);
+        for (int u = 0; u < nu; ++u) W.slot[(size_t)u] = u;
+        W.S = nu;
+        return W;
+    }
     const int TW = G.tw(), TL = G.tl(), C = 256 / G.xrow(), ZC = G.ucap % C;
     const int PAD = nu;  // the zero row, as a member id
     auto nbat = [&](int r) { return std::max(1, (rp[r + 1] - rp[r] + WSN_B - 1) / WSN_B); };
-    // (group key, member) for every running team's entry
-    std::vector<std::pair<int64_t, int>> mem;
+    // every running team's entry as (group key, member), bucketed by key
+    // (counting sort: keys are dense), then de-duplicated inside each group
+    // (one address reads once: broadcast)
     const int maxb = Rw.empty() ? 1 : nbat(Rw[0]) + 1;
+    const int nkeys = 8 * maxb * WSN_B * 4;
+    std::vector<int> kk, km;
+    kk.reserve(4096), km.reserve(4096);
     for (int q = 0; q < 8 && (size_t)q * TW < Rw.size(); ++q) {
         const int nt_q = (int)std::min<size_t>(TW, Rw.size() - (size_t)q * TW);
         for (int k = 0; k < nt_q; ++k) {
@@ -1294,17 +1304,30 @@ WsnSlots colour_wsn_slots(const WsnGeom &G, const int *rp, const int *ci, const 
             for (int b = 0; b < nbat(r); ++b)
                 for (int e = 0; e < WSN_B; ++e) {
                     const int el = WSN_B * b + e;
-                    const int64_t key = (((int64_t)q * maxb + b) * WSN_B + e) * 4 + lg;
-                    mem.emplace_back(key, el < rl ? pos[ci[rp[r] + el]] : PAD);
+                    kk.push_back(((q * maxb + b) * WSN_B + e) * 4 + lg);
+                    km.push_back(el < rl ? pos[ci[rp[r] + el]] : PAD);
                 }
         }
     }
-    std::sort(mem.begin(), mem.end());
-    mem.erase(std::unique(mem.begin(), mem.end()), mem.end());  // one address reads once (broadcast)
-    // groups as ranges of mem; per union row, the groups it is read in
-    std::vector<int> gstart;
-    for (size_t i = 0; i < mem.size(); ++i)
-        if (i == 0 || mem[i].first != mem[i - 1].first) gstart.push_back((int)i);
+    std::vector<int> kstart((size_t)nkeys + 1, 0);
+    for (int key : kk) ++kstart[(size_t)key + 1];
+    for (int i = 0; i < nkeys; ++i) kstart[(size_t)i + 1] += kstart[(size_t)i];
+    std::vector<int> memv(kk.size());
+    {
+        std::vector<int> at(kstart.begin(), kstart.end() - 1);
+        for (size_t i = 0; i < kk.size(); ++i) memv[(size_t)at[(size_t)kk[i]]++] = km[i];
+    }
+    // groups: the non-empty keys, members sorted and unique (PAD = nu last)
+    std::vector<int> gstart, mem;
+    mem.reserve(memv.size());
+    for (int key = 0; key < nkeys; ++key) {
+        const int a = kstart[(size_t)key], b = kstart[(size_t)key + 1];
+        if (a == b) continue;
+        std::sort(memv.begin() + a, memv.begin() + b);
+        gstart.push_back((int)mem.size());
+        for (int i = a; i < b; ++i)
+            if (i == a || memv[(size_t)i] != memv[(size_t)i - 1]) mem.push_back(memv[(size_t)i]);
+    }
     const int ng = (int)gstart.size();
     gstart.push_back((int)mem.size());
     W.groups = ng;
@@ -1312,13 +1335,13 @@ WsnSlots colour_wsn_slots(const WsnGeom &G, const int *rp, const int *ci, const 
     for (int g = 0; g < ng; ++g)
         for (int i = gstart[g]; i < gstart[g + 1]; ++i) {
             gof[(size_t)i] = g;
-            ++deg[(size_t)mem[(size_t)i].second];
+            ++deg[(size_t)mem[(size_t)i]];
         }
     std::vector<int> cptr((size_t)nu + 2, 0), cg((size_t)mem.size());
     for (int u = 0; u <= nu; ++u) cptr[(size_t)u + 1] = cptr[(size_t)u] + deg[(size_t)u];
     {
         std::vector<int> fill(cptr.begin(), cptr.end() - 1);
-        for (size_t i = 0; i < mem.size(); ++i) cg[(size_t)fill[(size_t)mem[i].second]++] = gof[i];
+        for (size_t i = 0; i < mem.size(); ++i) cg[(size_t)fill[(size_t)mem[i]]++] = gof[i];
     }
     auto model = [&](const std::vector<int> &col) {  // LDS cycles: per group its most-loaded colour
         int64_t cyc = 0;
@@ -1327,7 +1350,7 @@ WsnSlots colour_wsn_slots(const WsnGeom &G, const int *rp, const int *ci, const 
             std::fill(cnt.begin(), cnt.end(), 0);
             int mx = 0;
             for (int i = gstart[g]; i < gstart[g + 1]; ++i) {
-                const int u = mem[(size_t)i].second;
+                const int u = mem[(size_t)i];
                 mx = std::max(mx, ++cnt[(size_t)(u == PAD ? ZC : col[(size_t)u])]);
             }
             cyc += mx;
@@ -1351,19 +1374,22 @@ WsnSlots colour_wsn_slots(const WsnGeom &G, const int *rp, const int *ci, const 
     for (int c = 0; c < C; ++c) cap[(size_t)c] = std::min(want, (G.ucap - c + C - 1) / C);
     std::vector<int> cnt((size_t)ng * C, 0), col((size_t)nu, -1);
     for (int g = 0; g < ng; ++g)
-        if (mem[(size_t)gstart[g]].second == PAD || mem[(size_t)gstart[g + 1] - 1].second == PAD)
+        if (mem[(size_t)gstart[g + 1] - 1] == PAD)
             cnt[(size_t)g * C + ZC] = 1;  // (PAD sorts last in its group)
     std::vector<int> order((size_t)nu);
     for (int u = 0; u < nu; ++u) order[(size_t)u] = u;
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return deg[(size_t)a] > deg[(size_t)b]; });
     auto place = [&](int u) {
+        int cost[8] = {};
+        for (int i = cptr[(size_t)u]; i < cptr[(size_t)u + 1]; ++i) {
+            const int *cc = &cnt[(size_t)cg[(size_t)i] * C];
+            for (int c = 0; c < C; ++c) cost[c] += cc[c];
+        }
         int best = -1;
-        int64_t bc = 0;
         for (int c = 0; c < C; ++c) {
             if (used[(size_t)c] >= cap[(size_t)c]) continue;
-            int64_t cost = 0;
-            for (int i = cptr[(size_t)u]; i < cptr[(size_t)u + 1]; ++i) cost += cnt[(size_t)cg[(size_t)i] * C + c];
-            if (best < 0 || cost < bc || (cost == bc && used[(size_t)c] < used[(size_t)best])) best = c, bc = cost;
+            if (best < 0 || cost[c] < cost[best] || (cost[c] == cost[best] && used[(size_t)c] < used[(size_t)best]))
+                best = c;
         }
         if (best < 0) return false;
         col[(size_t)u] = best;
@@ -1414,8 +1440,18 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
     // 8 entries of room); the layout checks the real figure (splitting a tile
     // that still overflows, e.g. one holding empty rows, which own a batch)
     caps.ncap = G.ncap * frac_num / frac_den - 8;
+    // SMFV_PLAN_TIMING=1: the phases' host times on stderr (diagnostic)
+    static const bool timing = std::getenv("SMFV_PLAN_TIMING") != nullptr;
+    auto tick = [t = std::chrono::steady_clock::now()](const char *what) mutable {
+        const auto now = std::chrono::steady_clock::now();
+        if (timing)
+            std::fprintf(stderr, "[smfv wsn plan] %s %.1f ms\n", what,
+                         std::chrono::duration<double, std::milli>(now - t).count());
+        t = now;
+    };
     TileAnalysis T;
     analyse_tiles(m, n, rp, ci, T, caps);
+    tick("analyse_tiles");
 
     auto nbat = [&](int r) { return std::max(1, (rp[r + 1] - rp[r] + WSN_B - 1) / WSN_B); };
     auto by_length = [&](std::vector<int> &rows) {
@@ -1468,6 +1504,7 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
                                               std::max<int64_t>(N - cap * (8 - x), P.xcd[x - 1]));
     }
     const int nt = (int)N;
+    tick("tiles split");
     std::vector<int64_t> toff((size_t)nt + 1, 0);
     for (int t = 0; t < nt; ++t) toff[(size_t)t + 1] = toff[(size_t)t] + layout(tiles[(size_t)t]);
     P.ntiles = nt;
@@ -1495,7 +1532,7 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
         int *g = &P.grec[(size_t)t * WSN_GWORDS];
         int *l = &P.lrec[(size_t)t * LWD];
         // (r6) union rows in bank-coloured image slots (holes: X row 0, unread)
-        const WsnSlots SL = colour_wsn_slots(G, rp, ci, Rw, pos, nu, caps.wsn_colour);
+        const WsnSlots SL = colour_wsn_slots(G, rp, ci, Rw, pos, nu, caps.wsn_colour, !caps.wsn_model);
         for (int u = 0; u < nu; ++u) g[SL.slot[(size_t)u]] = ucols[(size_t)u];
         P.x_groups += SL.groups;
         P.x_cycles += SL.cycles;
@@ -1552,7 +1589,10 @@ bool build_wsn_plan_at(int m, int n, const int *rp, const int *ci, int kw, WsnPl
         P.union_rows += nu;
     }
     std::sort(P.direct.begin(), P.direct.end());
-    return verify_wsn_plan(m, n, rp, ci, P, err);
+    tick("layout");
+    const bool ok = verify_wsn_plan(m, n, rp, ci, P, err);
+    tick("verify");
+    return ok;
 }
 }  // namespace
 
@@ -1575,20 +1615,31 @@ bool build_wsn_plan(int m, int n, const int *rp, const int *ci, int kw, WsnPlan 
         return r;
     };
     bool any = false;
+    // (r6) the fractions are compared on first-use slots (the choice does not
+    // depend on the slot order); the winner alone is rebuilt with coloured
+    // slots (A/B: SMFV_WSN_FIRST_USE_SLOTS keeps first-use slots)
     TileCaps cs = caps;
-    if (std::getenv("SMFV_WSN_FIRST_USE_SLOTS")) cs.wsn_colour = false;  // (r6) A/B of the slot colouring
-    for (const auto &f : fr) {
+    const bool colour = caps.wsn_colour && !std::getenv("SMFV_WSN_FIRST_USE_SLOTS");
+    cs.wsn_colour = false;
+    int best = -1;
+    for (int i = 0; i < 6; ++i) {
         WsnPlan Q;
         std::string e;
-        if (!build_wsn_plan_at(m, n, rp, ci, kw, Q, &e, cs, f[0], f[1])) {
+        if (!build_wsn_plan_at(m, n, rp, ci, kw, Q, &e, cs, fr[i][0], fr[i][1])) {
             if (err && !any) *err = e;
             continue;
         }
         const bool better = !any || rounds(Q) < rounds(P) ||
                             (rounds(Q) == rounds(P) &&
                              (Q.ntiles < P.ntiles || (Q.ntiles == P.ntiles && Q.union_rows < P.union_rows)));
-        if (better) P = std::move(Q);
+        if (better) P = std::move(Q), best = i;
         any = true;
+    }
+    if (any && (colour || caps.wsn_model)) {
+        cs.wsn_colour = colour;
+        WsnPlan Q;
+        std::string e;
+        if (build_wsn_plan_at(m, n, rp, ci, kw, Q, &e, cs, fr[best][0], fr[best][1])) P = std::move(Q);
     }
     return any;
 }

@@ -146,6 +146,7 @@ struct TileCaps {
     // (r6) build_wsn_plan: union rows in bank-coloured image slots
     // (colour_wsn_slots, smfv_plan.cpp); false: first-use order
     bool wsn_colour = true;
+    bool wsn_model = false;        // (r6) also model the X reads' LDS cycles (WsnPlan::x_*; smfv_wsn_plan_analyse)
 };
 // Independent parts are analysed on up to 8 threads; analysis_threads > 0
 // caps that for analyses run on the calling thread (smfv_set_analysis_threads).

@@ -1045,6 +1045,40 @@ def test_live_values_full_size_and_contract(gpu):
         del g
 
 
+def test_live_values_x_over_4gib(gpu):
+    """(r6) A live-values tiled plan executed on an X spanning
+    4 GiB or more (n * ldx * 8; known only at execute) runs the untiled row
+    kernel on the same live values instead of failing: bit-identical to the
+    untiled plan, and to the snapshot plan (whose non-SADDR instance takes
+    such an X).  A 27-point stencil of 4,000 rows whose X has 16.8 M rows
+    (4.3 GB): its columns touch the first 4,000 only."""
+    B = smfv.gen_fem27(4000, 16, 16, 0.83, 7)
+    K = 32
+    n = (1 << 32) // (8 * K) + 1024
+    A = smfv.SparseMatrix(B.values, B.colIndices, B.rowPtr, B.numRows, n)
+    dA = smfv.DeviceCSR(A, gpu)
+    dX = torch.empty((n, K), dtype=torch.float64, device=gpu)
+    smfv.fill_x_hash(dX, 11)
+    live = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, live_values=True, tiles="force")
+    snap = smfv.SpmmPlan(smfv.Variant.ROWWISE, dA, K, tiles="force")
+    ref = smfv.SpmmPlan(smfv.Variant.SEQUENTIAL, dA, K, tiles="off")
+    assert live.stats()["live_values"] and live.stats()["tiled"]
+    Y = {k: torch.full((A.numRows, K), np.nan, dtype=torch.float64, device=gpu) for k in ("live", "snap", "ref")}
+    live.run(dX, Y["live"])
+    snap.run(dX, Y["snap"])
+    ref.run(dX, Y["ref"])
+    torch.cuda.synchronize()
+    assert torch.equal(Y["live"].view(torch.int64), Y["ref"].view(torch.int64))
+    assert torch.equal(Y["snap"].view(torch.int64), Y["ref"].view(torch.int64))
+    # the live values are read at every execute (no bind)
+    dA.values.mul_(-0.25)
+    live.run(dX, Y["live"])
+    ref.run(dX, Y["ref"])
+    torch.cuda.synchronize()
+    assert torch.equal(Y["live"].view(torch.int64), Y["ref"].view(torch.int64))
+    del dX
+
+
 @pytest.mark.parametrize("K", [4, 8])
 def test_narrow_team_tiles(gpu, K):
     """(r5) K = 4 / 8 windows take the narrow-team tiles (k_rows_wsn: K/2
