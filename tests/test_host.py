@@ -681,6 +681,13 @@ def test_narrow_team_plan_on_host():
         out = (ctypes.c_double * 9)()
         _lib.call("smfv_wsn_plan_analyse", r0, A.numRows if r1 is None else r1, A.numCols,
                   A.rowPtr.ctypes.data_as(ip), A.colIndices.ctypes.data_as(ip), kw, out)
+        # (r6) the X reads' modelled LDS cycles: conflict-free count <= the
+        # plan's bank-coloured slots < first-use slots (58 -> 45 % conflict
+        # cycles at K/p = 4 on the stencil stand-in)
+        groups, coloured, plain = out[6], out[7], out[8]
+        assert 0 < groups <= coloured <= plain, (kw, groups, coloured, plain)
+        if A.numRows == 121192:
+            assert (coloured - groups) / coloured < 0.9 * (plain - groups) / plain, (kw, coloured, plain)
         return [float(v) for v in out[:6]]
     A = smfv.inputs.cop20k_surrogate()
     for kw, rows in ((4, 256), (8, 128)):
