@@ -121,6 +121,8 @@ def measured_rank_traffic(config: str, p: int, rank: int, kernel: str):
     decomposition (profiles/pmc_traffic.json key '<config>@p<p>r<rank>',
     from a PMC run of `bench.py --rank-plans p --rank-only rank`: the same
     rank plan smfv_dist_plan_create gives that rank)."""
+    if p == 1:  # one rank: its plan is the whole matrix's (the N = 1 line's traffic)
+        return measured_traffic(config, kernel)
     return measured_traffic(f"{config}@p{p}r{rank}", kernel)
 
 
@@ -249,7 +251,7 @@ def cpu_baseline(A, K: int, variant: str, sample: str | None = None, budget_s: f
         sweep = {}
         for c in counts:
             # the reported point (the top rank count): median of 10 calls
-            t = _ref_run(A, K, tag, c, ref, 10 if c == counts[-1] and many else 3, budget_s * 6)
+            t = _ref_run(A, K, tag, c, ref, 10 if c == counts[-1] else 3, budget_s * 6)
             if t:
                 sweep[str(c)] = round(flops / t / 1e9, 4)
         nproc_point = None
@@ -267,7 +269,7 @@ def cpu_baseline(A, K: int, variant: str, sample: str | None = None, budget_s: f
                     "binding": "MPICH hydra " + " ".join(MPI_BIND) + " (one rank per core), -launcher fork",
                     "nproc_point": nproc_point,
                     "sample": f"{what}, reference {name} (SC sources, g++ -O3) under MPICH mpiexec -n {top}, "
-                              f"median of {10 if many else 3} calls incl. gather + FatVector rebuild"
+                              f"median of 10 calls incl. gather + FatVector rebuild"
                               f"{'; 1/2/4/8/16-rank sweep and the -O0 build beside it' if sweep_ranks else ''}"
                               f"{'; the 16-rank point (one GPU share) beside it' if many and not sweep_ranks else ''}; "
                               f"wall {time.time() - t0:.1f}s",
