@@ -576,6 +576,13 @@ def _graph_or_eager(step, steps: int, world: int):
 CPU_BASELINE_WAIT_S = 900.0  # the other ranks' wait while rank 0 times the CPU baseline (N > 1)
 
 
+def rendezvous_seconds(args, world: int) -> float:
+    """Deadline of the process-group rendezvous: the ranks other than 0 wait
+    there while rank 0 times the CPU baseline (N > 1)."""
+    extra = CPU_BASELINE_WAIT_S if world > 1 and not args.no_cpu_baseline else 0.0
+    return args.phase_timeout + extra
+
+
 def rank0_cpu_baseline(args, world: int, rank: int, dl, fn):
     """(r6) The CPU/MPI baseline beside EVERY line, N > 1 included
     (north_star: GFLOP/s at 1/2/4/8 GPUs alongside the CPU/MPI baseline):
@@ -638,7 +645,7 @@ def bench_rowpart(args, world: int, rank: int, local: int, K: int) -> None:
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
-    dl.enter("process group + RCCL communicator")
+    dl.enter("process group + RCCL communicator", seconds=rendezvous_seconds(args, world))
     if world > 1:
         dist.init_process_group("gloo")
     comm = D.Communicator.from_torch_distributed()
@@ -768,7 +775,8 @@ def bench_decomposed(args, world: int, rank: int, local: int, kind: str, K: int,
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))
     torch.cuda.set_device(dev)
-    dl.enter("process group + RCCL communicator")
+    # (the other ranks wait for rank 0's CPU baseline in this rendezvous)
+    dl.enter("process group + RCCL communicator", seconds=rendezvous_seconds(args, world))
     if world > 1:
         dist.init_process_group("gloo")  # control plane: barrier, max over ranks, RCCL id
     try:
