@@ -1002,6 +1002,43 @@ def test_live_values_odd_rows_and_block_end(gpu, K):
         assert same(Yb, Yref[r0:r1]), (r0, r1)
 
 
+@pytest.mark.parametrize("K", [32, 8])
+def test_live_values_poison_before_odd_rows(gpu, K):
+    """(r6) NaN and -inf as the LAST value of rows followed by rows that start
+    at odd CSR indices (whose value pairs are 8-byte aligned; an r6 variant
+    that started them one value early, 16-byte aligned, read exactly these
+    values into its first pair -- measured even and dropped,
+    profiles/r06/lead/): the poisoned rows are NaN, their neighbours bit-exact.
+    Row lengths 1..41, row blocks starting at odd and even CSR indices."""
+    rng = np.random.default_rng(200 + K)
+    m = n = 2600
+    lens = (np.arange(m) * 5) % 41 + 1
+    rp = np.zeros(m + 1, np.int64)
+    rp[1:] = np.cumsum(lens)
+    ci = np.concatenate([np.sort(rng.choice(np.arange(max(0, i - 50), min(n, i + 50)), L, replace=False))
+                         for i, L in enumerate(lens)]).astype(np.int32)
+    va = rng.uniform(-1, 1, ci.size)
+    lead_rows = [r for r in range(1, m) if rp[r] % 2 == 1 and lens[r] % 8]
+    assert len(lead_rows) > 500
+    poison = lead_rows[:60:2]
+    va[rp[poison[::2]] - 1] = np.nan   # the last value of the row before
+    va[rp[poison[1::2]] - 1] = -np.inf
+    A = mat(rp.astype(np.int32), ci, va, m, n)
+    X = rng.uniform(-1, 1, (n, K))
+    Yref = oracle.spmm("sequential", A.rowPtr, A.colIndices, A.values, X)
+
+    def same(Y, Yr):
+        nan = np.isnan(Yr)
+        return np.array_equal(np.isnan(Y), nan) and np.array_equal(bits(Y)[~nan], bits(Yr)[~nan])
+    assert np.all(np.isfinite(Yref[poison]))  # the poisoned values belong to the rows before
+    plan, Y = _live_run(A, X, gpu)
+    assert plan.stats()["live_values"] and plan.stats()["tiled"]
+    assert same(Y, Yref)
+    for r0, r1 in ((poison[3], 1900), (poison[4] + 1, m), (1, m - 3)):
+        plan, Yb = _live_run(A, X, gpu, rows=(r0, r1))
+        assert same(Yb, Yref[r0:r1]), (r0, r1, int(rp[r0]) % 2)
+
+
 def test_live_values_full_size_and_contract(gpu):
     """The cop20k_A stand-ins at K = 32 and the stencil at K = 128: live
     plans bit-identical; values changed IN PLACE with no bind are seen by the
