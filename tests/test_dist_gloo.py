@@ -1,4 +1,4 @@
-"""Multi-process (world_size 2 and 3, gloo, CPU) test of the distributed
+"""Multi-process (world_size 2, 3 and (r6) 5, gloo, CPU) test of the distributed
 exchange: each rank takes its part from the NATIVE plan (smfv_dist_plan --
 the function the GPU path runs), computes it with the oracle, then replays
 the NATIVE exchange schedule (smfv_dist_exchange_ops: the exact list of
@@ -147,7 +147,7 @@ def _worker(rank, p, port, variant, mode, q):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-@pytest.mark.parametrize("p", [2, 3])
+@pytest.mark.parametrize("p", [2, 3, 5])
 @pytest.mark.parametrize("variant", [1, 2, 3])
 def test_gloo_exchange(variant, p, mode):
     ctx = mp.get_context("spawn")
