@@ -1,6 +1,7 @@
 """(r4) Every rank plan of a p-GPU decomposition at FULL size, on one device:
-p in {2, 4, 8}, ROWWISE / COLUMNWISE / NONZERO, K = 32, on both cop20k_A
-stand-ins (the 27-point-stencil surrogate and the irregular k-NN one).
+p in {2, 3, 4, 5, 8} (r6: 3 and 5 split K = 32 into uneven column windows),
+ROWWISE / COLUMNWISE / NONZERO, K = 32, on both cop20k_A stand-ins (the
+27-point-stencil surrogate and the irregular k-NN one).
 
 Each rank r runs its share through the product's rank plan
 (smfv_dist_plan_create_rank: the partition of SC/...RowWise.cpp:26-29,
@@ -50,7 +51,7 @@ PARTS = [(smfv.Variant.ROWWISE, "balanced", 1), (smfv.Variant.ROWWISE, "referenc
          (smfv.Variant.NONZERO, "balanced", 1)]
 
 
-@pytest.mark.parametrize("p", [2, 4, 8])
+@pytest.mark.parametrize("p", [2, 3, 4, 5, 8])
 @pytest.mark.parametrize("variant,partition,chunks", PARTS)
 def test_rank_plans_full_size(gpu, standin, p, variant, partition, chunks):
     name, A, X, Yseq, absY, dA, dX = standin
