@@ -602,8 +602,8 @@ def rank0_cpu_baseline(args, world: int, rank: int, dl, fn):
                  seconds=args.phase_timeout + CPU_BASELINE_WAIT_S)
     cpu = fn()
     if cpu is not None and world > 1:
-        cpu["note_n_gpus"] = (f"beside the {world}-GPU line: {cpu.get('cores')} MPI ranks = 16 per GPU "
-                              f"(capped at the {len(os.sched_getaffinity(0))} CPUs this process may use)")
+        cpu["note_n_gpus"] = (f"beside the {world}-GPU line: {cpu.get('cores')} MPI ranks (16 per GPU = "
+                              f"{16 * world}, capped at the {len(os.sched_getaffinity(0))} CPUs this process may use)")
     return cpu
 
 
